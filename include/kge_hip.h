@@ -1,0 +1,214 @@
+/*
+ * kge_hip.h -- C-ABI of libkge_hip.so, the MI355X (gfx950) native training
+ * step for knowledge-graph embeddings.
+ *
+ * This is the drop-in boundary for the hot path of
+ * melissakou/knowledge-graph-embedding (pure-Python TF 2.5; no native code of
+ * its own). Every entry point below replaces a Python/TF call site of the
+ * reference; the citation is given per entry point. The host side that binds
+ * it is the Python package `KGE` (ctypes, knowledge-graph-embedding_amd/KGE/_hip.py);
+ * INTEGRATION.md shows the binding.
+ *
+ * Rules of the ABI
+ *  - Plain C types only: device pointers, sizes, enums. No torch / HIP types
+ *    in signatures; streams are passed as `void*` (a hipStream_t, NULL = the
+ *    legacy default stream).
+ *  - The library never allocates device memory: the caller passes a
+ *    workspace of at least kge_step_workspace_bytes() bytes.
+ *  - Calls are stream-ordered, re-entrant and never throw. They return a
+ *    kge_status; kge_last_error() gives a thread-local message.
+ *  - Device-side range violations (entity / relation ids out of range) are
+ *    recorded in the caller's `status` word (KGE_ERANGE) and the offending
+ *    triple is skipped; the host checks the word at its next sync.
+ *  - Tables are fp32, row-major, with a row stride `ld` >= cols (floats).
+ */
+#ifndef KGE_HIP_H
+#define KGE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KGE_ABI_VERSION 1
+
+typedef enum kge_status {
+  KGE_OK = 0,
+  KGE_EINVAL = 1,            /* bad argument (reference: Python assert / TF InvalidArgument) */
+  KGE_ERANGE = 2,            /* id out of range (reference: TF gather InvalidArgument on CPU) */
+  KGE_EHIP = 3,              /* HIP runtime error */
+  KGE_ENOMEM_WORKSPACE = 4,  /* workspace smaller than kge_step_workspace_bytes() */
+  KGE_EUNSUPPORTED = 5       /* combination not implemented natively */
+} kge_status;
+
+/* models: KGE/models/translating_based/<Model>.py, KGE/models/semantic_based/<Model>.py */
+enum {
+  KGE_MODEL_TRANSE = 0,   /* TransE.py:127-174   */
+  KGE_MODEL_TRANSH = 1,   /* TransH.py:149-213   */
+  KGE_MODEL_TRANSR = 2,   /* TransR.py:154-211   */
+  KGE_MODEL_TRANSD = 3,   /* TransD.py:170-242   */
+  KGE_MODEL_ROTATE = 4,   /* RotatE.py:126-181   */
+  KGE_MODEL_DISTMULT = 5, /* DistMult.py:118-167 */
+  KGE_MODEL_RESCAL = 6    /* RESCAL.py:140-200   */
+};
+
+/* score kinds: KGE/score.py */
+enum {
+  KGE_SCORE_LP = 0,       /* LpDistance(p)    score.py:49-63 */
+  KGE_SCORE_LP_POW = 1,   /* LpDistancePow(p) score.py:65-76 */
+  KGE_SCORE_DOT = 2       /* Dot()            score.py:78-89 */
+};
+
+/* loss kinds: KGE/loss.py */
+enum {
+  KGE_LOSS_HINGE = 0,     /* PairwiseHingeLoss                    loss.py:49-82   */
+  KGE_LOSS_LOGISTIC = 1,  /* PairwiseLogisticLoss                 loss.py:85-113  */
+  KGE_LOSS_BCE = 2,       /* BinaryCrossEntropyLoss               loss.py:116-143 */
+  KGE_LOSS_SANS = 3,      /* SelfAdversarialNegativeSamplingLoss  loss.py:146-182 */
+  KGE_LOSS_SQERR = 4      /* SquareErrorLoss                      loss.py:185-204 */
+};
+
+/* corrupt_side: BaseModel.py:332-408 */
+enum { KGE_SIDE_H = 0, KGE_SIDE_T = 1, KGE_SIDE_HT = 2 };
+
+/* index dtype of triples / sampled ids (int64 from numpy, int32 from CSV:
+ * data_utils.py:182, ns_strategy.py:57) */
+enum { KGE_IDX_I32 = 0, KGE_IDX_I64 = 1 };
+
+/* negative samplers: KGE/ns_strategy.py */
+enum {
+  KGE_SAMPLER_UNIFORM = 0, /* UniformStrategy ns_strategy.py:39-64            */
+  KGE_SAMPLER_TYPED = 1,   /* TypedStrategy   ns_strategy.py:94-132, utils.py:11-16 */
+  KGE_SAMPLER_GIVEN = 2    /* negatives supplied by the caller (neg_ids input) */
+};
+
+/* optimizer applied by the step (BaseModel.py:325-328) */
+enum { KGE_OPT_NONE = 0, KGE_OPT_SGD = 1 };
+
+typedef struct kge_table {
+  float* data;   /* device pointer, row-major                    */
+  int64_t rows;
+  int64_t cols;  /* floats per row                               */
+  int64_t ld;    /* row stride in floats (>= cols)               */
+} kge_table;
+
+/*
+ * Counter-based sampler state. Draw n of a call uses Philox4x32-10 with
+ * key = (seed lo, seed hi) and counter = (block lo, block hi, plane lo,
+ * plane hi), block = n / P, P = 4 (int32 ids: one 32-bit word per draw) or
+ * 2 (int64 ids: words 2q | 2q+1 << 32), and maps bits -> bits % range as
+ * TF's UniformDistribution does. A 'h+t' step uses plane `offset` for the
+ * head side and `offset + 1` for the tail side, i.e. exactly two standalone
+ * kge_sample() calls (the reference calls the strategy h-side first,
+ * BaseModel.py:353-356).
+ */
+typedef struct kge_sampler_desc {
+  int32_t kind;               /* KGE_SAMPLER_*                                  */
+  int32_t idx_dtype;          /* KGE_IDX_*                                      */
+  uint64_t seed;
+  uint64_t offset;            /* counter plane of the first side                */
+  int64_t n_entities;         /* uniform: pool length (E unless `pool` given)   */
+  const void* pool;           /* uniform: optional pool [n_entities] (idx_dtype); NULL = range(E) */
+  const int32_t* ent_type;    /* typed: [E] type id of each entity              */
+  const int32_t* type_offsets;/* typed: [n_types+1] CSR offsets                 */
+  const int32_t* type_members;/* typed: [E] entity ids grouped by type, ascending*/
+  const int32_t* pos_in_type; /* typed: [E] position of entity in its group     */
+  int32_t n_types;
+  int32_t _pad;
+} kge_sampler_desc;
+
+/* Standalone sampler: NegativeSampler.__call__(X, negative_ratio, side)
+ * (ns_strategy.py:39-64 uniform, :94-132 typed). out[n*negative_ratio]. */
+typedef struct kge_sample_desc {
+  kge_sampler_desc sampler;
+  const void* X;              /* [n,3] idx_dtype                                */
+  int64_t n;
+  int32_t side;               /* KGE_SIDE_H or KGE_SIDE_T                       */
+  int32_t negative_ratio;
+  void* out;                  /* [n*negative_ratio] idx_dtype                   */
+  int32_t* status;            /* device status word (nullable)                  */
+} kge_sample_desc;
+
+/*
+ * One training (or validation) step: KGEModel.__run_single_batch
+ * (BaseModel.py:293-330) for the built-in models and plugins:
+ *   negative sampling (:316, :332-408) -> _constraint_loss (:319) ->
+ *   score_hrt(pos), score_hrt(neg) (:320-321) -> loss_fn (:322-323) ->
+ *   gradients (:326) -> clip_by_norm(g, clip_norm) per variable (:327) ->
+ *   optimizer.apply_gradients (:328).
+ * Variables (per-variable clipping, norm2_out order): 0 ent_emb, 1 the main
+ * relation table (rel_emb / rel_inter), 2 rel_aux (rel_hyper / rel_proj),
+ * 3 ent_aux (ent_proj).
+ */
+typedef struct kge_step_desc {
+  int32_t abi_version;        /* KGE_ABI_VERSION                                */
+  int32_t model;              /* KGE_MODEL_*                                    */
+  kge_table ent;              /* ent_emb [E, d]  (RotatE: [E, 2d] = [E,d,2])    */
+  kge_table rel;              /* rel_emb / rel_inter [R, d_rel]                 */
+  kge_table ent_aux;          /* TransD ent_proj [E, d]                         */
+  kge_table rel_aux;          /* TransH rel_hyper [R,d]; TransD rel_proj [R,d_rel] */
+  int32_t dim;                /* entity embedding size d                        */
+  int32_t dim_rel;            /* relation embedding size                        */
+
+  const void* pos;            /* positives [batch, 3] (h, r, t)                 */
+  int32_t idx_dtype;          /* KGE_IDX_*                                      */
+  int32_t batch;
+  int32_t negative_ratio;
+  int32_t corrupt_side;       /* KGE_SIDE_*                                     */
+
+  kge_sampler_desc sampler;
+  void* neg_ids;              /* [batch*K_eff] idx_dtype: input for GIVEN, output otherwise (nullable) */
+
+  int32_t score_kind;         /* KGE_SCORE_*                                    */
+  float score_p;              /* 1, 2 or +inf                                   */
+  int32_t loss_kind;          /* KGE_LOSS_*                                     */
+  float margin;
+  float temperature;
+  float batch_scale;          /* global-batch normalisation (world size), 1 on one device */
+  int32_t constraint;         /* model's `constraint` flag                      */
+  float constraint_weight;
+  float rotate_limit;         /* RotatE self.limit (RotatE.py:93)              */
+
+  int32_t optimizer;          /* KGE_OPT_NONE (validation step) or KGE_OPT_SGD  */
+  float lr;
+  float clip_norm;            /* 5.0 in the reference (BaseModel.py:327)        */
+
+  float* loss_out;            /* [1] batch loss (device)                        */
+  float* loss_accum;          /* [1] += batch loss (device, nullable)           */
+  float* pos_score_out;       /* [batch] (nullable)                             */
+  float* neg_score_out;       /* [batch*K_eff] (nullable)                       */
+  float* norm2_out;           /* [4] per-variable gradient norm^2 (nullable)    */
+  int32_t* status;            /* device status word (nullable)                  */
+
+  void* workspace;
+  uint64_t workspace_bytes;
+} kge_step_desc;
+
+/* ABI version compiled into the library. */
+int32_t kge_abi_version(void);
+
+/* Thread-local message for the last non-OK status. */
+const char* kge_last_error(void);
+
+/* Workspace needed by kge_step for this descriptor (0 on error). */
+uint64_t kge_step_workspace_bytes(const kge_step_desc* d);
+
+/* One training / validation step (see kge_step_desc). */
+kge_status kge_step(const kge_step_desc* d, void* stream);
+
+/* Standalone negative sampling (ns_strategy.py:39-64, :94-132). */
+kge_status kge_sample(const kge_sample_desc* d, void* stream);
+
+/* Row constraints over a whole table (constraint.py:4-31, :70-99):
+ * kind 0 = normalized_embeddings(p=2, value), 1 = clip_constraint(p=2, value).
+ * Used by the models' _constraint_loss (TransE.py:171-172, TransR.py:207-209,
+ * TransD.py:238-240) and _init_embeddings (TransE.py:108-109). */
+kge_status kge_constrain_rows(kge_table t, int32_t kind, float value, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KGE_HIP_H */

@@ -1,0 +1,146 @@
+"""ctypes binding of ``libkge_hip.so`` (C-ABI declared in ``include/kge_hip.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` into
+``KGE/_lib/libkge_hip.so``. ``lib()`` raises ``RuntimeError`` when it cannot be
+loaded: the fused path never falls back silently.
+"""
+
+import ctypes
+import os
+import threading
+
+import torch
+
+ABI_VERSION = 1
+
+KGE_OK, KGE_EINVAL, KGE_ERANGE, KGE_EHIP, KGE_ENOMEM_WORKSPACE, KGE_EUNSUPPORTED = range(6)
+
+MODEL_TRANSE, MODEL_TRANSH, MODEL_TRANSR, MODEL_TRANSD, MODEL_ROTATE, MODEL_DISTMULT, MODEL_RESCAL = range(7)
+SIDE_H, SIDE_T, SIDE_HT = range(3)
+IDX_I32, IDX_I64 = range(2)
+SAMPLER_UNIFORM, SAMPLER_TYPED, SAMPLER_GIVEN = range(3)
+OPT_NONE, OPT_SGD = range(2)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libkge_hip.so")
+
+
+class kge_table(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("rows", ctypes.c_int64), ("cols", ctypes.c_int64),
+                ("ld", ctypes.c_int64)]
+
+
+class kge_sampler_desc(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("idx_dtype", ctypes.c_int32), ("seed", ctypes.c_uint64),
+                ("offset", ctypes.c_uint64), ("n_entities", ctypes.c_int64), ("pool", ctypes.c_void_p),
+                ("ent_type", ctypes.c_void_p), ("type_offsets", ctypes.c_void_p),
+                ("type_members", ctypes.c_void_p), ("pos_in_type", ctypes.c_void_p),
+                ("n_types", ctypes.c_int32), ("_pad", ctypes.c_int32)]
+
+
+class kge_sample_desc(ctypes.Structure):
+    _fields_ = [("sampler", kge_sampler_desc), ("X", ctypes.c_void_p), ("n", ctypes.c_int64),
+                ("side", ctypes.c_int32), ("negative_ratio", ctypes.c_int32), ("out", ctypes.c_void_p),
+                ("status", ctypes.c_void_p)]
+
+
+class kge_step_desc(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_int32), ("model", ctypes.c_int32),
+        ("ent", kge_table), ("rel", kge_table), ("ent_aux", kge_table), ("rel_aux", kge_table),
+        ("dim", ctypes.c_int32), ("dim_rel", ctypes.c_int32),
+        ("pos", ctypes.c_void_p), ("idx_dtype", ctypes.c_int32), ("batch", ctypes.c_int32),
+        ("negative_ratio", ctypes.c_int32), ("corrupt_side", ctypes.c_int32),
+        ("sampler", kge_sampler_desc), ("neg_ids", ctypes.c_void_p),
+        ("score_kind", ctypes.c_int32), ("score_p", ctypes.c_float),
+        ("loss_kind", ctypes.c_int32), ("margin", ctypes.c_float), ("temperature", ctypes.c_float),
+        ("batch_scale", ctypes.c_float),
+        ("constraint", ctypes.c_int32), ("constraint_weight", ctypes.c_float),
+        ("rotate_limit", ctypes.c_float),
+        ("optimizer", ctypes.c_int32), ("lr", ctypes.c_float), ("clip_norm", ctypes.c_float),
+        ("loss_out", ctypes.c_void_p), ("loss_accum", ctypes.c_void_p),
+        ("pos_score_out", ctypes.c_void_p), ("neg_score_out", ctypes.c_void_p),
+        ("norm2_out", ctypes.c_void_p), ("status", ctypes.c_void_p),
+        ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64),
+    ]
+
+
+EXPORTS = ("kge_abi_version", "kge_last_error", "kge_step_workspace_bytes", "kge_step", "kge_sample",
+           "kge_constrain_rows")
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load the library and declare prototypes (no GPU call is made)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise RuntimeError(
+                "libkge_hip.so not found at %s: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                % path)
+        L = ctypes.CDLL(path)
+        L.kge_abi_version.restype = ctypes.c_int32
+        L.kge_last_error.restype = ctypes.c_char_p
+        L.kge_step_workspace_bytes.restype = ctypes.c_uint64
+        L.kge_step_workspace_bytes.argtypes = [ctypes.POINTER(kge_step_desc)]
+        L.kge_step.restype = ctypes.c_int
+        L.kge_step.argtypes = [ctypes.POINTER(kge_step_desc), ctypes.c_void_p]
+        L.kge_sample.restype = ctypes.c_int
+        L.kge_sample.argtypes = [ctypes.POINTER(kge_sample_desc), ctypes.c_void_p]
+        L.kge_constrain_rows.restype = ctypes.c_int
+        L.kge_constrain_rows.argtypes = [kge_table, ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]
+        if L.kge_abi_version() != ABI_VERSION:
+            raise RuntimeError("libkge_hip.so ABI %d != binding %d" % (L.kge_abi_version(), ABI_VERSION))
+        _lib = L
+        return L
+
+
+def lib():
+    return load()
+
+
+def check(status, what):
+    """Turn a kge_status into the reference's exception types."""
+    if status == KGE_OK:
+        return
+    msg = "%s: %s" % (what, lib().kge_last_error().decode(errors="replace"))
+    if status in (KGE_EINVAL, KGE_ERANGE):
+        raise ValueError(msg)
+    if status == KGE_EUNSUPPORTED:
+        raise NotImplementedError(msg)
+    raise RuntimeError(msg)
+
+
+def check_device_status(status_tensor, what="kge"):
+    """Raise if a kernel recorded a device-side error in the status word."""
+    code = int(status_tensor.item())
+    if code == KGE_OK:
+        return
+    status_tensor.zero_()
+    if code == KGE_ERANGE:
+        raise ValueError("%s: entity / relation id out of range (device check)" % what)
+    if code == KGE_EINVAL:
+        raise ValueError("%s: a typed-sampling pool is empty after removing the entity itself "
+                         "(np.random.choice on an empty pool, utils.py:11-16)" % what)
+    raise RuntimeError("%s: device status %d" % (what, code))
+
+
+def table(t):
+    """kge_table view of a 2-D fp32 tensor (row stride from the tensor)."""
+    if t.dtype != torch.float32 or not t.is_cuda:
+        raise ValueError("embedding tables must be float32 CUDA tensors")
+    t2 = t.view(t.shape[0], -1) if t.dim() != 2 else t   # never copies
+    if t2.stride(1) != 1:
+        raise ValueError("embedding tables must be row-major (unit column stride)")
+    return kge_table(t2.data_ptr(), t2.shape[0], t2.shape[1], t2.stride(0))
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def stream_handle(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,184 @@
+"""Data utilities (reference ``KGE/data_utils.py:12-196``).
+
+``index_kg`` / ``convert_kg_to_index`` / ``train_test_split_no_unseen`` /
+``calculate_data_size`` keep the reference's behaviour on numpy arrays and CSV
+folders. ``set_tf_iterator`` is replaced by a device-resident batcher with the
+same stream semantics as ``tf.data ... shuffle(n, seed,
+reshuffle_each_iteration=True).repeat().batch(B)`` (``data_utils.py:176-196``):
+every batch has exactly ``batch_size`` rows and batches straddle epoch
+boundaries; CSV folders give int32 triples, numpy input keeps its dtype
+(int64), as ``CsvDataset(record_defaults=[tf.int32]*3)`` /
+``from_tensor_slices`` do.
+"""
+
+import logging
+import os
+
+import numpy as np
+import pandas as pd
+import torch
+
+from .utils import check_path_exist_and_create
+
+
+def index_kg(kg_data):
+    """Index a KG (``data_utils.py:23-62``).
+
+    numpy input: sorted ``np.unique`` of entities / relations. CSV folder:
+    first-appearance order over files (``pd.unique``), files in
+    ``os.listdir`` order.
+    """
+    if isinstance(kg_data, np.ndarray):
+        entities = list(np.unique(np.append(kg_data[:, 0], kg_data[:, 2])))
+        relations = list(np.unique(kg_data[:, 1]))
+    else:
+        ent_parts, rel_parts = [], []
+        for f in os.listdir(kg_data):
+            tmp = pd.read_csv(os.path.join(kg_data, f), header=None, dtype=str)
+            ent_parts += [tmp.iloc[:, 0], tmp.iloc[:, 2]]
+            rel_parts.append(tmp.iloc[:, 1])
+        entities = list(pd.unique(pd.concat(ent_parts, ignore_index=True))) if ent_parts else []
+        relations = list(pd.unique(pd.concat(rel_parts, ignore_index=True))) if rel_parts else []
+
+    ent2ind = {e: i for i, e in enumerate(entities)}
+    ind2ent = [e for e in entities]
+    rel2ind = {r: i for i, r in enumerate(relations)}
+    ind2rel = [r for r in relations]
+    return {"ent2ind": ent2ind, "ind2ent": ind2ent, "rel2ind": rel2ind, "ind2rel": ind2rel}
+
+
+def convert_kg_to_index(kg_data, ent2ind, rel2ind):
+    """Map string triples to ids (``data_utils.py:65-99``)."""
+    if isinstance(kg_data, np.ndarray):
+        h = list(map(ent2ind.get, list(kg_data[:, 0])))
+        r = list(map(rel2ind.get, list(kg_data[:, 1])))
+        t = list(map(ent2ind.get, list(kg_data[:, 2])))
+        return np.array([h, r, t]).T
+    filenames = os.listdir(kg_data)
+    check_path_exist_and_create(kg_data + "_indexed")
+    for f in filenames:
+        tmp = pd.read_csv(kg_data + "/" + f, header=None, dtype=str)
+        tmp.iloc[:, 0] = tmp.iloc[:, 0].map(ent2ind)
+        tmp.iloc[:, 1] = tmp.iloc[:, 1].map(rel2ind)
+        tmp.iloc[:, 2] = tmp.iloc[:, 2].map(ent2ind)
+        tmp.to_csv(kg_data + "_indexed/" + f, index=False, header=False)
+    logging.info("indexed_kg has been save to %s" % kg_data + "_indexed")
+
+
+def train_test_split_no_unseen(X, test_size, seed):
+    """Split so every test entity / relation is also in train (``data_utils.py:102-159``)."""
+    if isinstance(test_size, float):
+        test_size = int(len(X) * test_size)
+
+    e, e_cnt = np.unique(np.append(X[:, 0], X[:, 2]), return_counts=True)
+    r, r_cnt = np.unique(X[:, 1], return_counts=True)
+    e_dict = dict(zip(e, e_cnt))
+    r_dict = dict(zip(r, r_cnt))
+
+    test_id = np.array([], dtype=int)
+    train_id = np.arange(len(X))
+    loop_count = 0
+    max_loop = len(X) * 10
+    rnd = np.random.RandomState(seed)
+    while len(test_id) < test_size:
+        i = rnd.choice(train_id)
+        if e_dict[X[i, 0]] > 1 and r_dict[X[i, 1]] > 1 and e_dict[X[i, 2]] > 1:
+            e_dict[X[i, 0]] -= 1
+            r_dict[X[i, 1]] -= 1
+            e_dict[X[i, 2]] -= 1
+            test_id = np.unique(np.append(test_id, i))
+        loop_count += 1
+        if loop_count == max_loop:
+            logging.error("Cannot split a test set with desired size, please reduce the test size")
+            return
+    train_id = np.setdiff1d(train_id, test_id)
+    return X[train_id], X[test_id]
+
+
+def calculate_data_size(X):
+    """Number of triples in an array or CSV folder (``data_utils.py:162-173``)."""
+    if isinstance(X, str):
+        total = 0
+        for f in os.listdir(X):
+            total += len(pd.read_csv(os.path.join(X, f), header=None))
+        return total
+    return len(X)
+
+
+def load_triples(data):
+    """numpy / tensor / CSV folder -> host int tensor [n, 3].
+
+    CSV folders are read as int32 (the reference's CsvDataset defaults,
+    ``data_utils.py:182``); arrays keep an integer dtype (numpy default int64).
+    """
+    if isinstance(data, str):
+        parts = [pd.read_csv(os.path.join(data, f), header=None, dtype=np.int32).values
+                 for f in sorted(os.listdir(data))]
+        arr = np.concatenate(parts, axis=0) if parts else np.zeros((0, 3), np.int32)
+        return torch.from_numpy(np.ascontiguousarray(arr.astype(np.int32)))
+    if isinstance(data, torch.Tensor):
+        return data.detach().cpu()
+    arr = np.asarray(data)
+    if arr.dtype.kind not in "iu":
+        arr = arr.astype(np.int64)
+    if arr.dtype not in (np.int32, np.int64):
+        arr = arr.astype(np.int64)
+    return torch.from_numpy(np.ascontiguousarray(arr))
+
+
+class DeviceBatcher:
+    """Device-resident ``shuffle -> repeat -> batch`` stream.
+
+    The triples live on ``device``; each epoch draws a fresh permutation from a
+    host generator seeded once with ``seed`` (reshuffle_each_iteration), and
+    ``next()`` returns the next ``batch_size`` rows of the endless stream, so a
+    batch may span two epochs exactly like ``repeat().batch()``.
+    """
+
+    def __init__(self, data, batch_size, shuffle, seed=None, device=None):
+        host = load_triples(data)
+        self.n = host.shape[0]
+        if self.n == 0:
+            raise ValueError("empty triple set")
+        self.batch_size = int(batch_size)
+        self.shuffle = shuffle
+        self.device = device if device is not None else torch.device("cpu")
+        self.data = host.to(self.device)
+        self.gen = torch.Generator()
+        if seed is not None:
+            self.gen.manual_seed(int(seed))
+        else:
+            self.gen.seed()
+        self._order = None
+        self._pos = 0
+
+    def _next_epoch(self):
+        if self.shuffle:
+            perm = torch.randperm(self.n, generator=self.gen)
+        else:
+            perm = torch.arange(self.n)
+        self._order = perm.to(self.device)
+        self._pos = 0
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        pieces = []
+        need = self.batch_size
+        while need > 0:
+            if self._order is None or self._pos >= self.n:
+                self._next_epoch()
+            take = min(need, self.n - self._pos)
+            pieces.append(self._order[self._pos:self._pos + take])
+            self._pos += take
+            need -= take
+        idx = pieces[0] if len(pieces) == 1 else torch.cat(pieces)
+        return self.data.index_select(0, idx)
+
+
+def set_tf_iterator(data, batch_size, shuffle, buffer_size=None, seed=None, device=None):
+    """Drop-in for ``set_tf_iterator`` (``data_utils.py:176-196``)."""
+    if shuffle:
+        assert buffer_size is not None, "buffer_size must be given when shuffle is True"
+    return DeviceBatcher(data, batch_size, shuffle, seed=seed, device=device)

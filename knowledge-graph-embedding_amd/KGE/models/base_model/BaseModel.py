@@ -1,0 +1,368 @@
+"""Base module for KGE models (reference ``KGE/models/base_model/BaseModel.py``).
+
+``KGEModel`` keeps the reference's public surface -- ``train`` (:58-190),
+``evaluate`` (:578-618), ``get_rank`` (:620-654), ``score_hrt`` (:410-430),
+``restore_model_weights`` (:656-666) -- and its per-batch step
+(``__run_single_batch``, :293-330), which is dispatched by ``KGE.engine`` to
+the fused HIP step (``libkge_hip.so``) or, for user-defined plugins, to the
+eager autograd path with the same TF-2.5 semantics.
+
+Deviations from the reference, all documented in DESIGN.md:
+  * ``train`` without ``val_X`` works (the reference fails at :148).
+  * ``get_rank`` counts in int64 (the reference's int16 overflows for E > 32767).
+  * ``restore_model_weights`` checks the given weights (the reference calls
+    ``_check_model_weights()`` without its argument, :665).
+  * per-batch losses stay on the device; the host reads one value per epoch
+    (the reference syncs every batch with ``.numpy()``, :330).
+  * TensorBoard summaries are written as JSON lines under ``log_path``.
+"""
+
+import datetime
+import json
+import logging
+import os
+
+import numpy as np
+import torch
+
+from ... import engine
+from ... import optimizers as _opt
+from ...data_utils import calculate_data_size, set_tf_iterator
+from ...metrics import (geometric_mean_rank, harmonic_mean_rank, hits_at_k, mean_rank, mean_reciprocal_rank,
+                        median_rank, std_rank)
+from ...ns_strategy import TypedStrategy, UniformStrategy
+
+logging.getLogger().setLevel(logging.INFO)
+
+
+class KGEModel:
+    """Base class for KGE models (``BaseModel.py:23-56``)."""
+
+    _fused_model_id = None
+
+    def __init__(self, embedding_params, negative_ratio, corrupt_side, loss_fn, ns_strategy, n_workers):
+        assert corrupt_side in ['h+t', 'h', 't'], "Invalid corrupt_side, valid options: 'h+t', 'h', 't'"
+        self.embedding_params = embedding_params
+        self.negative_ratio = negative_ratio
+        self.corrupt_side = corrupt_side
+        self.loss_fn = loss_fn
+        self.ns_strategy = ns_strategy
+        self._n_workers = n_workers
+        self._model_weights_initial = None
+        self._tape = None
+        self._batch_scale = 1.0
+        self._fused = None
+        self._optimizer = None
+        self.metadata = None
+
+    # ------------------------------------------------------------ train
+    def train(self, train_X, val_X, metadata, epochs, batch_size, early_stopping_rounds=None,
+              model_weights_initial=None, restore_best_weight=True, optimizer="Adam", seed=None,
+              log_path="./logs", log_projector=False):
+        """Train the model (``BaseModel.py:58-190``)."""
+        self.metadata = metadata
+        self.batch_size = batch_size
+        self._model_weights_initial = model_weights_initial
+        self._optimizer = optimizer
+        self.seed = seed
+        self.log_path = log_path
+
+        logging.info("[%s] Preparing for training..." % str(datetime.datetime.now()))
+        train_iter, val_iter = self._prepare_for_train(train_X=train_X, val_X=val_X)
+        train_loss_history, val_loss_history = [], []
+        patience_count = 0
+        self.best_step = None
+
+        logging.info("[%s] Start Training..." % str(datetime.datetime.now()))
+        for i in range(epochs):
+            train_loss = torch.zeros((), dtype=torch.float64, device=self._device)
+            val_loss = torch.zeros((), dtype=torch.float64, device=self._device)
+            for b in range(self._batch_count_train):
+                train_loss += self._run_single_batch(next(train_iter), is_train=True)
+                if val_iter is not None and b < self._batch_count_val:
+                    val_loss += self._run_single_batch(next(val_iter), is_train=False)
+            self._check_device_status()
+            train_loss = float(train_loss) / self._batch_count_train
+            train_loss_history.append(train_loss)
+            self._log_scalar("train", train_loss, i)
+            if val_iter is not None:
+                val_loss = float(val_loss) / self._batch_count_val
+                val_loss_history.append(val_loss)
+                self._log_scalar("validation", val_loss, i)
+                logging.info("epoch: %i, train loss: %f, valid loss: %f" % (i, train_loss, val_loss))
+            else:
+                logging.info("epoch: %i, train loss: %f" % (i, train_loss))
+
+            if early_stopping_rounds is not None:
+                assert val_X is not None, "val_X should be given if want to check early stopping."
+                early_stop, patience_count = self._check_early_stopping(
+                    val_loss_history, "larger", patience_count, early_stopping_rounds, i, restore_best_weight)
+                if early_stop:
+                    logging.info("[%s] Val loss does not improve within %i iterations, trigger early stopping."
+                                 % (str(datetime.datetime.now()), early_stopping_rounds))
+                    break
+            else:
+                self._save_checkpoint()
+        self.train_loss_history = train_loss_history
+        self.val_loss_history = val_loss_history
+        if log_projector:
+            self._log_embeddings_projector(log_path)
+        logging.info("[%s] Finished training!" % str(datetime.datetime.now()))
+
+    def _prepare_for_train(self, train_X, val_X):
+        """``BaseModel.py:192-278``: batch counts, iterators, init, optimizer, sampler."""
+        self._device = engine.device()
+        n_train = calculate_data_size(train_X)
+        self._batch_count_train = int(np.ceil(n_train / self.batch_size))
+        train_iter = set_tf_iterator(train_X, self.batch_size, shuffle=True, buffer_size=n_train,
+                                     seed=self.seed, device=self._device)
+        if val_X is not None:
+            n_val = calculate_data_size(val_X)
+            self._batch_count_val = int(np.ceil(n_val / self.batch_size))
+            val_iter = set_tf_iterator(val_X, self.batch_size, shuffle=False, device=self._device)
+        else:
+            self._batch_count_val = 0
+            val_iter = None
+
+        self._init_embeddings(seed=self.seed)
+        self._to_device()
+        self._optimizer = _opt.get(self._optimizer)
+        check_path = self.log_path
+        os.makedirs(check_path, exist_ok=True)
+
+        if self.ns_strategy is UniformStrategy:
+            self.ns_strategy = UniformStrategy(sample_pool=np.arange(len(self.metadata["ind2ent"])),
+                                               seed=self.seed)
+        elif self.ns_strategy is TypedStrategy:
+            self.metadata["type2inds"] = {}
+            for t in np.unique(self.metadata["ind2type"]):
+                indices = [i for (i, ti) in enumerate(self.metadata["ind2type"]) if ti == t]
+                self.metadata["type2inds"][t] = np.array(indices)
+            self.ns_strategy = TypedStrategy(pool=None, metadata={
+                "type2inds": self.metadata["type2inds"], "ind2type": self.metadata["ind2type"]}, seed=self.seed)
+        self._fused = None
+        return train_iter, val_iter
+
+    def _to_device(self):
+        dev = getattr(self, "_device", None) or engine.device()
+        self._device = dev
+        for k, w in list(self.model_weights.items()):
+            if not isinstance(w, torch.Tensor):
+                w = torch.as_tensor(np.asarray(w), dtype=torch.float32)
+            self.model_weights[k] = w.detach().to(device=dev, dtype=torch.float32).contiguous()
+
+    # ------------------------------------------------------------ step
+    def _run_single_batch(self, batch_data, is_train):
+        """One batch (``BaseModel.py:293-330``); returns the loss as a device scalar."""
+        opt = self._optimizer if is_train else None
+        reason = engine.fused_plan(self, opt)
+        if reason is None:
+            if self._fused is None:
+                self._fused = engine.FusedStep(self)
+            return self._fused(batch_data, is_train, opt).clone().reshape(()).to(torch.float64)
+        if engine.backend() != "eager":
+            engine.warn_once((type(self).__name__, reason), "eager plugin path: %s" % reason)
+        return engine.eager_step(self, batch_data, is_train, opt).to(torch.float64)
+
+    def _check_device_status(self):
+        if self._fused is not None:
+            self._fused.check_status()
+
+    def _negative_sampling(self, X):
+        """``BaseModel.py:332-358``."""
+        if self.corrupt_side == 'h':
+            return self._corrupt_h(X, self.negative_ratio, self.ns_strategy)
+        if self.corrupt_side == 't':
+            return self._corrupt_t(X, self.negative_ratio, self.ns_strategy)
+        h = self._corrupt_h(X, self.negative_ratio // 2, self.ns_strategy)
+        t = self._corrupt_t(X, self.negative_ratio // 2, self.ns_strategy)
+        return torch.cat([h, t], dim=-1).reshape(-1, 3)
+
+    def _corrupt_h(self, X, negative_ratio, strategy):
+        """``BaseModel.py:360-383``."""
+        h = strategy(X, negative_ratio=negative_ratio, side="h").to(X.device)
+        r = torch.repeat_interleave(X[:, 1], negative_ratio)
+        t = torch.repeat_interleave(X[:, 2], negative_ratio)
+        return torch.stack([h, r, t], dim=1)
+
+    def _corrupt_t(self, X, negative_ratio, strategy):
+        """``BaseModel.py:385-408``."""
+        s = strategy(X, negative_ratio=negative_ratio, side="t").to(X.device)
+        h = torch.repeat_interleave(X[:, 0], negative_ratio)
+        r = torch.repeat_interleave(X[:, 1], negative_ratio)
+        return torch.stack([h, r, s], dim=1)
+
+    # ------------------------------------------------------------ plugin helpers
+    def _ids(self, x):
+        dev = self.model_weights["ent_emb"].device
+        if isinstance(x, torch.Tensor):
+            return x.to(dev).to(torch.int64)
+        return torch.as_tensor(np.asarray(x), dtype=torch.int64, device=dev)
+
+    def _lookup(self, name, idx):
+        """``tf.nn.embedding_lookup``; under a training tape each lookup is a
+        separate leaf so its gradient is one IndexedSlices block."""
+        w = self.model_weights[name]
+        idx = self._ids(idx)
+        if self._tape is None:
+            return w[idx]
+        flat = idx.reshape(-1)
+        leaf = w.detach().index_select(0, flat).requires_grad_(True)
+        self._tape.records.append((name, flat, leaf))
+        return leaf.reshape(tuple(idx.shape) + tuple(w.shape[1:]))
+
+    def _assign(self, name, value):
+        """``Variable.assign`` inside ``_constraint_loss`` (no gradient)."""
+        with torch.no_grad():
+            self.model_weights[name].copy_(value)
+
+    def score_hrt(self, h, r, t):
+        """Resolve ``None`` to every entity (``BaseModel.py:410-430``)."""
+        assert not (h is None and t is None), "h and t should not be None simultaneously"
+        n = len(self.metadata["ind2ent"])
+        if h is None:
+            r, t = self._ids(r), self._ids(t)
+            assert r.dim() == 0 and t.dim() == 0
+            h = torch.arange(n, device=r.device)
+        if t is None:
+            h, r = self._ids(h), self._ids(r)
+            assert h.dim() == 0 and r.dim() == 0
+            t = torch.arange(n, device=h.device)
+        return self._ids(h), self._ids(r), self._ids(t)
+
+    def _init_embeddings(self, seed):
+        raise NotImplementedError("subclass of KGEModel should implement _init_embeddings()")
+
+    def _constraint_loss(self, X):
+        raise NotImplementedError("subclass of KGEModel should implement _constraint_loss()")
+
+    def _check_model_weights(self, model_weights):
+        raise NotImplementedError("subclass of KGEModel should implement _check_model_weights()")
+
+    def _uniform(self, shape, limit, gen):
+        dev = engine.device()
+        return (torch.rand(shape, generator=gen, dtype=torch.float32) * 2 - 1).mul_(limit).to(dev)
+
+    def _generator(self, seed):
+        g = torch.Generator()
+        if seed is not None:
+            g.manual_seed(int(seed))
+        else:
+            g.seed()
+        return g
+
+    def _initial_weights(self):
+        """Copy of ``model_weights_initial`` as device fp32 tensors."""
+        dev = engine.device()
+        out = {}
+        for k, v in self._model_weights_initial.items():
+            t = v if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
+            out[k] = t.detach().to(device=dev, dtype=torch.float32).clone().contiguous()
+        return out
+
+    # ------------------------------------------------------------ logging / ckpt
+    def _log_scalar(self, split, value, step):
+        path = os.path.join(self.log_path, "scalar", split)
+        os.makedirs(path, exist_ok=True)
+        with open(os.path.join(path, "loss.jsonl"), "a") as f:
+            f.write(json.dumps({"step": step, "loss": value}) + "\n")
+
+    def _save_checkpoint(self):
+        """``CheckpointManager(max_to_keep=1).save()`` (``BaseModel.py:248-253``)."""
+        os.makedirs(self.log_path, exist_ok=True)
+        path = os.path.join(self.log_path, "ckpt.pt")
+        torch.save({k: v.detach().cpu() for k, v in self.model_weights.items()}, path)
+        return path
+
+    def _restore_checkpoint(self):
+        path = os.path.join(self.log_path, "ckpt.pt")
+        saved = torch.load(path, weights_only=True)
+        with torch.no_grad():
+            for k, v in saved.items():
+                self.model_weights[k].copy_(v.to(self.model_weights[k].device))
+
+    def _check_early_stopping(self, metric_history, magnitude, patience_now, patience_max, step,
+                              restore_best_weight=True):
+        """``BaseModel.py:485-540``."""
+        if step == 0:
+            self._save_checkpoint()
+            self.best_step = step
+            return False, patience_now
+        assert magnitude in ["larger", "smaller"], "magnitude must be 'larger' or 'smaller'"
+        if self.best_step is None:
+            self.best_step = step
+        if magnitude == "larger":
+            flag = metric_history[step] >= metric_history[self.best_step]
+        else:
+            flag = metric_history[step] <= metric_history[self.best_step]
+        if flag:
+            patience_now += 1
+        else:
+            patience_now = 0
+            self.best_step = step
+            self._save_checkpoint()
+        if patience_now == patience_max:
+            if restore_best_weight:
+                self._restore_checkpoint()
+            return True, patience_now
+        return False, patience_now
+
+    def _log_embeddings_projector(self, log_path):
+        """Projector artefacts (``BaseModel.py:542-576``) as TSV files."""
+        def write(path, rows):
+            with open(path, "w") as f:
+                for x in rows:
+                    f.write("{}\n".format(x))
+        write(os.path.join(log_path, "ent_metadata.tsv"), self.metadata["ind2ent"])
+        ent = self.model_weights["ent_emb"].detach().cpu().reshape(len(self.metadata["ind2ent"]), -1).numpy()
+        np.savetxt(os.path.join(log_path, "ent_emb.tsv"), ent, delimiter="\t")
+        if self.model_weights.get("rel_emb") is not None:
+            write(os.path.join(log_path, "rel_metadata.tsv"), self.metadata["ind2rel"])
+            rel = self.model_weights["rel_emb"].detach().cpu().reshape(len(self.metadata["ind2rel"]), -1).numpy()
+            np.savetxt(os.path.join(log_path, "rel_emb.tsv"), rel, delimiter="\t")
+
+    # ------------------------------------------------------------ evaluation
+    def evaluate(self, eval_X, corrupt_side, positive_X=None):
+        """``BaseModel.py:578-618``."""
+        X = np.asarray(eval_X) if not isinstance(eval_X, torch.Tensor) else eval_X.cpu().numpy()
+        ranks = [self.get_rank(X[k], positive_X, corrupt_side) for k in range(len(X))]
+        return {
+            "mean_rank": mean_rank(ranks),
+            "mean_reciprocal_rank": mean_reciprocal_rank(ranks),
+            "median_rank": median_rank(ranks),
+            "geometric_mean_rank": geometric_mean_rank(ranks),
+            "harmonic_mean_rank": harmonic_mean_rank(ranks),
+            "std_rank": std_rank(ranks),
+            "hit@1": hits_at_k(ranks, k=1),
+            "hit@3": hits_at_k(ranks, k=3),
+            "hit@10": hits_at_k(ranks, k=10),
+        }
+
+    def get_rank(self, x, positive_X, corrupt_side):
+        """Rank of one triple among all corruptions (``BaseModel.py:620-654``):
+        ``sum(scores > pos_score) + 1`` with filtered positives set to -inf."""
+        x = np.asarray(x.cpu() if isinstance(x, torch.Tensor) else x).reshape(-1)
+        with torch.no_grad():
+            if corrupt_side == "h":
+                filter_side, corrupt = 2, 0
+                scores = self.score_hrt(h=None, r=x[1], t=x[2])
+            elif corrupt_side == "t":
+                filter_side, corrupt = 0, 2
+                scores = self.score_hrt(h=x[0], r=x[1], t=None)
+            else:
+                raise ValueError("corrupt_side must be 'h' or 't'")
+            scores = scores.reshape(-1).clone()
+            if positive_X is not None:
+                P = np.asarray(positive_X.cpu() if isinstance(positive_X, torch.Tensor) else positive_X)
+                mask = (P[:, 1] == x[1]) & (P[:, filter_side] == x[filter_side])
+                positive_e = torch.as_tensor(P[mask, corrupt].astype(np.int64), device=scores.device)
+                scores[positive_e] = -np.inf
+            pos_score = self.score_hrt(x[0:1], x[1:2], x[2:3]).reshape(())
+            return np.int64(int(torch.sum(scores > pos_score).item()) + 1)
+
+    def restore_model_weights(self, model_weights):
+        """``BaseModel.py:656-666`` (argument checked)."""
+        self._check_model_weights(model_weights)
+        self.model_weights = model_weights
+        self._to_device()
+        self._fused = None

@@ -1,0 +1,37 @@
+"""Misc helpers (reference ``KGE/utils.py:6-25``)."""
+
+import os
+import stat
+
+import numpy as np
+
+
+def check_path_exist_and_create(path):
+    """Recreate ``path`` empty (``utils.py:6-9``)."""
+    if os.path.exists(path):
+        rmtree(path)
+    os.makedirs(path)
+
+
+def ns_with_same_type(x, metadata, negative_ratio):
+    """Host restatement of ``utils.py:11-16``: ``negative_ratio`` draws (with
+    replacement, numpy global RNG) from ``type2inds[ind2type[x]]`` minus ``x``.
+
+    Kept for API compatibility; the fused path draws the same distribution on
+    device with the counter-based sampler (``ns_strategy.TypedStrategy``).
+    """
+    sample_pool = metadata["type2inds"][metadata["ind2type"][x]]
+    sample_pool = np.delete(sample_pool, np.where(sample_pool == x), axis=0)
+    return np.random.choice(sample_pool, size=negative_ratio)
+
+
+def rmtree(top):
+    """Remove a directory tree, forcing write permission (``utils.py:18-25``)."""
+    for root, dirs, files in os.walk(top, topdown=False):
+        for name in files:
+            filename = os.path.join(root, name)
+            os.chmod(filename, stat.S_IWUSR)
+            os.remove(filename)
+        for name in dirs:
+            os.rmdir(os.path.join(root, name))
+    os.rmdir(top)

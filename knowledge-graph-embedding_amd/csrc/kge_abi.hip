@@ -1,0 +1,324 @@
+// C-ABI layer of libkge_hip.so: descriptor validation, launch geometry,
+// workspace layout and the standalone sampler / constraint kernels.
+// Never throws across the ABI; errors -> kge_status + kge_last_error().
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "kge_step.h"
+
+using namespace kge;
+
+namespace {
+
+thread_local std::string g_err;
+
+kge_status fail(kge_status s, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return s;
+}
+
+kge_status hip_check(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(KGE_EHIP, "%s: %s", what, hipGetErrorString(e));
+  return KGE_OK;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
+inline int next_pow2(int64_t x) { int p = 1; while (p < x) p <<= 1; return p; }
+inline bool aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
+
+constexpr int kWaves = 4;
+constexpr int kUCap = 4096;   // update kernel: LDS list capacity (entries)
+
+struct Plan {
+  StepArgs A;
+  StepGeom G;
+  int sk;
+  uint64_t ws_bytes;
+  // workspace offsets
+  uint64_t o_ids, o_coef, o_snap, o_gpos, o_part, o_sorted, o_starts;
+};
+
+int score_sk(int kind, float p) {
+  if (kind == KGE_SCORE_DOT) return SK_DOT;
+  if (std::isinf(p)) return SK_PINF;
+  return p == 1.f ? SK_P1 : SK_P2;
+}
+
+kge_status check_table(const kge_table& t, const char* name, int64_t cols) {
+  if (!t.data) return fail(KGE_EINVAL, "%s: null data pointer", name);
+  if (t.rows <= 0) return fail(KGE_EINVAL, "%s: rows must be > 0 (got %lld)", name, (long long)t.rows);
+  if (t.cols != cols)
+    return fail(KGE_EINVAL, "%s: expected %lld columns, got %lld", name, (long long)cols, (long long)t.cols);
+  if (t.ld < t.cols) return fail(KGE_EINVAL, "%s: ld (%lld) < cols", name, (long long)t.ld);
+  return KGE_OK;
+}
+
+kge_status make_plan(const kge_step_desc* d, Plan* pl) {
+  if (!d) return fail(KGE_EINVAL, "null descriptor");
+  if (d->abi_version != KGE_ABI_VERSION)
+    return fail(KGE_EINVAL, "abi_version %d != library %d", d->abi_version, KGE_ABI_VERSION);
+  const int model = d->model;
+  if (model != KGE_MODEL_TRANSE && model != KGE_MODEL_DISTMULT && model != KGE_MODEL_ROTATE)
+    return fail(KGE_EUNSUPPORTED, "model %d has no fused kernel in this build", model);
+  if (d->dim <= 0) return fail(KGE_EINVAL, "dim must be > 0");
+  const int64_t entc = model == KGE_MODEL_ROTATE ? 2 * (int64_t)d->dim : d->dim;
+  const int64_t relc = d->dim;
+  kge_status s;
+  if ((s = check_table(d->ent, "ent_emb", entc))) return s;
+  if ((s = check_table(d->rel, model == KGE_MODEL_DISTMULT ? "rel_inter" : "rel_emb", relc))) return s;
+  if (d->batch < 0) return fail(KGE_EINVAL, "batch must be >= 0");
+  if (d->negative_ratio < 0) return fail(KGE_EINVAL, "negative_ratio must be >= 0");
+  if (d->corrupt_side < KGE_SIDE_H || d->corrupt_side > KGE_SIDE_HT)
+    return fail(KGE_EINVAL, "Invalid corrupt_side, valid options: 'h+t', 'h', 't'");
+  if (d->idx_dtype != KGE_IDX_I32 && d->idx_dtype != KGE_IDX_I64)
+    return fail(KGE_EINVAL, "idx_dtype must be KGE_IDX_I32 or KGE_IDX_I64");
+  if (d->batch > 0 && !d->pos) return fail(KGE_EINVAL, "null positive triples");
+  if (d->loss_kind < KGE_LOSS_HINGE || d->loss_kind > KGE_LOSS_SQERR)
+    return fail(KGE_EINVAL, "unknown loss kind %d", d->loss_kind);
+  if (d->score_kind < KGE_SCORE_LP || d->score_kind > KGE_SCORE_DOT)
+    return fail(KGE_EINVAL, "unknown score kind %d", d->score_kind);
+  const float p = d->score_p;
+  if (d->score_kind != KGE_SCORE_DOT && !(p == 1.f || p == 2.f || std::isinf(p)))
+    return fail(KGE_EUNSUPPORTED, "fused Lp score supports p in {1, 2, inf} (got %g)", (double)p);
+  if (model == KGE_MODEL_ROTATE && d->score_kind == KGE_SCORE_DOT)
+    return fail(KGE_EUNSUPPORTED, "RotatE with Dot() yields a complex score");
+  if (model == KGE_MODEL_ROTATE && !(d->rotate_limit > 0.f))
+    return fail(KGE_EINVAL, "RotatE rotate_limit must be > 0");
+  if (d->optimizer != KGE_OPT_NONE && d->optimizer != KGE_OPT_SGD)
+    return fail(KGE_EUNSUPPORTED, "optimizer %d has no fused kernel in this build", d->optimizer);
+  if (d->optimizer == KGE_OPT_SGD && !(d->clip_norm > 0.f)) return fail(KGE_EINVAL, "clip_norm must be > 0");
+  if (!d->loss_out) return fail(KGE_EINVAL, "null loss_out");
+  const kge_sampler_desc& sm = d->sampler;
+  if (sm.kind == KGE_SAMPLER_GIVEN) {
+    if (d->batch > 0 && d->negative_ratio > 0 && !d->neg_ids) return fail(KGE_EINVAL, "GIVEN sampler needs neg_ids");
+  } else if (sm.kind == KGE_SAMPLER_UNIFORM) {
+    if (sm.n_entities <= 0) return fail(KGE_EINVAL, "uniform sampler: empty pool");
+  } else if (sm.kind == KGE_SAMPLER_TYPED) {
+    if (!sm.ent_type || !sm.type_offsets || !sm.type_members || !sm.pos_in_type || sm.n_types <= 0)
+      return fail(KGE_EINVAL, "typed sampler: missing type tables");
+  } else {
+    return fail(KGE_EINVAL, "unknown sampler kind %d", sm.kind);
+  }
+  if (sm.idx_dtype != d->idx_dtype && sm.kind != KGE_SAMPLER_GIVEN)
+    return fail(KGE_EINVAL, "sampler idx_dtype must match triples");
+
+  Plan& P = *pl;
+  StepArgs& A = P.A;
+  A = StepArgs{};
+  const int K = d->negative_ratio;
+  const int Kside = d->corrupt_side == KGE_SIDE_HT ? K / 2 : K;
+  const int Keff = d->corrupt_side == KGE_SIDE_HT ? 2 * Kside : K;
+  const int64_t B = d->batch;
+
+  // fragment geometry
+  int vec;
+  const bool a16 = aligned(d->ent.data, 16) && aligned(d->rel.data, 16);
+  if (model == KGE_MODEL_ROTATE) {
+    vec = (entc % 4 == 0 && d->ent.ld % 4 == 0 && relc % 2 == 0 && d->rel.ld % 2 == 0 && a16) ? 4 : 2;
+    if (vec == 2 && !(d->ent.ld % 2 == 0 && aligned(d->ent.data, 8)))
+      return fail(KGE_EINVAL, "RotatE ent_emb must be 8-byte aligned with even row stride");
+  } else {
+    vec = (entc % 4 == 0 && relc % 4 == 0 && d->ent.ld % 4 == 0 && d->rel.ld % 4 == 0 && a16) ? 4 : 1;
+  }
+  const int64_t rowlen = std::max(entc, relc);
+  const int nc = (int)ceil_div(rowlen, 64 * vec);
+  if (nc > 4)
+    return fail(KGE_EUNSUPPORTED, "row of %lld floats exceeds the fused kernel's %d", (long long)rowlen, 256 * vec);
+  const int ncp = nc <= 1 ? 1 : nc <= 2 ? 2 : 4;
+
+  int nP = Keff >= 128 ? 1 : std::max(1, std::min(64, 256 / std::max(Keff, 1)));
+  nP = (int)std::max<int64_t>(1, std::min<int64_t>(nP, B / 256));
+  const int64_t nWG = std::max<int64_t>(1, ceil_div(B, nP));
+  const int64_t slotmax = (int64_t)nP * (Keff + 2);
+  if (slotmax > 65535) return fail(KGE_EUNSUPPORTED, "negative_ratio %d too large for one workgroup", K);
+  if (nWG > 65535) return fail(KGE_EUNSUPPORTED, "batch %lld too large (max %d workgroups)", (long long)B, 65535);
+  const int sortpad = next_pow2(slotmax);
+  if (sortpad > 8192) return fail(KGE_EUNSUPPORTED, "negative_ratio %d too large (LDS sort)", K);
+
+  const int64_t E = d->ent.rows, R = d->rel.rows;
+  const int64_t T = B * (Keff + 2);
+  int64_t Pb = std::max<int64_t>(1, std::min<int64_t>({ceil_div(T, 256), E, 65535}));
+  const int64_t bs = ceil_div(E, Pb);
+  Pb = ceil_div(E, bs);
+
+  const int FL = 64 * vec * ncp;
+  const int Kpad = (int)round_up(Keff + 1, 4);
+  const int idpad = (int)round_up((int64_t)nP * Keff, 4);
+  P.G.vec = vec;
+  P.G.nc = ncp;
+  P.G.nWG = (int)nWG;
+  P.G.gridU = (int)(Pb + ceil_div(R, kWaves));
+  P.G.lds_score = (size_t)kWaves * 3 * FL * 4 + 4 * (size_t)Kpad * 4 + (size_t)idpad * 4 + 64 * 4 +
+                  (size_t)sortpad * 8 + (size_t)nP * 3 * 8;
+  P.G.lds_update = (size_t)kUCap * 8 + 264 * 4 + (size_t)kWaves * FL * 4;
+  if (P.G.lds_score > 160 * 1024) return fail(KGE_EUNSUPPORTED, "LDS budget exceeded");
+  P.sk = score_sk(d->score_kind, p);
+
+  A.ent = TabView{d->ent.data, d->ent.ld, (int32_t)entc, E};
+  A.rel = TabView{d->rel.data, d->rel.ld, (int32_t)relc, R};
+  A.pos = d->pos;
+  A.i64 = d->idx_dtype == KGE_IDX_I64;
+  A.train = d->optimizer != KGE_OPT_NONE;
+  A.given = sm.kind == KGE_SAMPLER_GIVEN;
+  A.pw = d->score_kind == KGE_SCORE_LP_POW;
+  A.rel_half = model == KGE_MODEL_ROTATE;
+  A.B = B;
+  A.Keff = Keff;
+  A.Kside = Kside;
+  A.side_mode = d->corrupt_side;
+  A.smp = make_sampler_view(sm);
+  A.smp.i64 = A.i64;
+  A.neg_user = d->neg_ids;
+  A.loss_kind = d->loss_kind;
+  A.margin = d->margin;
+  A.temperature = d->temperature;
+  const double bg = (double)B * (d->batch_scale > 0.f ? d->batch_scale : 1.f);
+  A.inv_b = (float)(1.0 / bg);
+  A.inv_bk = (float)(1.0 / (bg * Keff));
+  A.limit = d->rotate_limit;
+  A.rel_reg = (model == KGE_MODEL_DISTMULT && d->constraint) ? d->constraint_weight : 0.f;
+  A.lr = d->lr;
+  A.clip_norm = d->clip_norm;
+  A.nP = nP;
+  A.nWG = (int32_t)nWG;
+  A.Kpad = Kpad;
+  A.idpad = idpad;
+  A.sortpad = sortpad;
+  A.slotmax = (int32_t)slotmax;
+  A.P = (int32_t)Pb;
+  A.bs = bs;
+  A.ucap = kUCap;
+  A.snap_cols = (int32_t)entc;
+  A.gcols = (int32_t)rowlen;
+  A.rel_gcols = (int32_t)relc;
+  A.loss_out = d->loss_out;
+  A.loss_accum = d->loss_accum;
+  A.pos_score_out = d->pos_score_out;
+  A.neg_score_out = d->neg_score_out;
+  A.norm2_out = d->norm2_out;
+  A.status = d->status;
+
+  uint64_t off = 0;
+  auto take = [&](uint64_t bytes) { const uint64_t o = off; off += round_up((int64_t)bytes, 256); return o; };
+  P.o_ids = take((uint64_t)B * Keff * 4);
+  P.o_coef = take((uint64_t)B * Keff * 8);
+  P.o_snap = take((uint64_t)B * 3 * entc * 4);
+  P.o_gpos = take((uint64_t)B * 3 * rowlen * 4);
+  P.o_part = take((uint64_t)nWG * 8 * 4);
+  P.o_sorted = take((uint64_t)nWG * slotmax * 8);
+  P.o_starts = take((uint64_t)nWG * (Pb + 1) * 4);
+  P.ws_bytes = std::max<uint64_t>(off, 256);
+  return KGE_OK;
+}
+
+// ------------------------------------------------------------ sampler kernel
+__global__ __launch_bounds__(256) void sample_kernel(SamplerView s, const void* X, int64_t n, int side,
+                                                      int K, void* out, int64_t E, int32_t* status) {
+  const int64_t total = n * (int64_t)K;
+  int err = 0;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = q / K;
+    int64_t e = 0;
+    const int64_t x = load_idx(X, i * 3 + (side == KGE_SIDE_H ? 0 : 2), s.i64);
+    if (s.kind == KGE_SAMPLER_TYPED && (x < 0 || x >= E)) err = KGE_ERANGE;
+    else {
+      e = sample_entity(s, s.offset, (uint64_t)q, x, &err);
+      if (e < 0) e = 0;
+    }
+    store_idx(out, q, e, s.i64);
+  }
+  if (err) set_status(status, err);
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t kge_abi_version(void) { return KGE_ABI_VERSION; }
+
+const char* kge_last_error(void) { return g_err.c_str(); }
+
+uint64_t kge_step_workspace_bytes(const kge_step_desc* d) {
+  Plan P;
+  if (make_plan(d, &P) != KGE_OK) return 0;
+  return P.ws_bytes;
+}
+
+kge_status kge_step(const kge_step_desc* d, void* stream) {
+  Plan P;
+  kge_status s = make_plan(d, &P);
+  if (s != KGE_OK) return s;
+  if (d->workspace_bytes < P.ws_bytes || !d->workspace)
+    return fail(KGE_ENOMEM_WORKSPACE, "workspace of %llu bytes < required %llu",
+                (unsigned long long)d->workspace_bytes, (unsigned long long)P.ws_bytes);
+  hipStream_t st = (hipStream_t)stream;
+  StepArgs& A = P.A;
+  unsigned char* ws = (unsigned char*)d->workspace;
+  A.ids = (int32_t*)(ws + P.o_ids);
+  A.coef = (float2*)(ws + P.o_coef);
+  A.snap = (float*)(ws + P.o_snap);
+  A.gpos = (float*)(ws + P.o_gpos);
+  A.part = (float*)(ws + P.o_part);
+  A.sorted = (uint64_t*)(ws + P.o_sorted);
+  A.starts = (int32_t*)(ws + P.o_starts);
+
+  // _constraint_loss assigns before scoring (BaseModel.py:319)
+  const bool renorm = d->constraint && (d->model == KGE_MODEL_TRANSE || d->model == KGE_MODEL_DISTMULT);
+  if (renorm) {
+    const int64_t blocks = std::min<int64_t>(ceil_div(d->ent.rows, kWaves), 4096);
+    hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, d->ent.data,
+                       d->ent.rows, (int32_t)d->ent.cols, d->ent.ld, 0, 1.0f);
+  }
+  if (d->batch == 0) {
+    (void)hipMemsetAsync(d->loss_out, 0, sizeof(float), st);
+    return hip_check("kge_step(empty batch)");
+  }
+  s = launch_step_elementwise(A, P.G, d->model, P.sk, st);
+  if (s != KGE_OK) return fail(s, "no kernel instance for model %d / score %d", d->model, P.sk);
+  return hip_check("kge_step");
+}
+
+kge_status kge_sample(const kge_sample_desc* d, void* stream) {
+  if (!d) return fail(KGE_EINVAL, "null descriptor");
+  const kge_sampler_desc& sm = d->sampler;
+  if (sm.kind != KGE_SAMPLER_UNIFORM && sm.kind != KGE_SAMPLER_TYPED)
+    return fail(KGE_EINVAL, "kge_sample: sampler kind must be UNIFORM or TYPED");
+  if (d->side != KGE_SIDE_H && d->side != KGE_SIDE_T) return fail(KGE_EINVAL, "side must be 'h' or 't'");
+  if (d->n < 0 || d->negative_ratio < 0) return fail(KGE_EINVAL, "negative sizes");
+  if (sm.n_entities <= 0) return fail(KGE_EINVAL, "sampler: n_entities must be > 0");
+  if (sm.kind == KGE_SAMPLER_TYPED &&
+      (!sm.ent_type || !sm.type_offsets || !sm.type_members || !sm.pos_in_type || sm.n_types <= 0))
+    return fail(KGE_EINVAL, "typed sampler: missing type tables");
+  const int64_t total = d->n * (int64_t)d->negative_ratio;
+  if (total == 0) return KGE_OK;
+  if (!d->X || !d->out) return fail(KGE_EINVAL, "null X / out");
+  SamplerView v = make_sampler_view(sm);
+  const int64_t blocks = std::min<int64_t>(ceil_div(total, 256), 8192);
+  const int64_t E = sm.n_entities;
+  hipLaunchKernelGGL(sample_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, v, d->X,
+                     d->n, d->side, d->negative_ratio, d->out, E, d->status);
+  return hip_check("kge_sample");
+}
+
+kge_status kge_constrain_rows(kge_table t, int32_t kind, float value, void* stream) {
+  if (!t.data || t.rows < 0 || t.cols <= 0 || t.ld < t.cols) return fail(KGE_EINVAL, "bad table");
+  if (kind != 0 && kind != 1) return fail(KGE_EINVAL, "kind must be 0 (normalize) or 1 (clip)");
+  if (t.rows == 0) return KGE_OK;
+  const int64_t blocks = std::min<int64_t>(ceil_div(t.rows, kWaves), 4096);
+  hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, t.data,
+                     t.rows, (int32_t)t.cols, t.ld, kind, value);
+  return hip_check("kge_constrain_rows");
+}
+
+}  // extern "C"

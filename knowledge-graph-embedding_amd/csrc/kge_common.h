@@ -1,0 +1,211 @@
+// Device-side building blocks shared by the KGE kernels (gfx950 / CDNA4).
+//
+//  * Philox4x32-10 counter-based generator + the TF UniformDistribution
+//    mapping (bits % range) used by the negative samplers.
+//  * wave64 reductions.
+//  * Row fragments: a table row of `cols` floats is spread over the 64 lanes
+//    of ONE wave, lane l holding elements [(c*64 + l)*VEC, +VEC) for chunk
+//    c < NC; VEC = 4 gives one 16-byte load per lane per chunk, i.e. a whole
+//    800-byte row (d = 200) per wave-instruction.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/kge_hip.h"
+
+#define KGE_WAVE 64
+
+namespace kge {
+
+// ---------------------------------------------------------------- Philox
+struct PhiloxKey { uint32_t k0, k1; };
+
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, PhiloxKey k) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k.k0 += 0x9E3779B9u; k.k1 += 0xBB67AE85u; }
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.k0, lo1, hi0 ^ c.w ^ k.k1, lo0);
+  }
+  return c;
+}
+
+// Draw n of counter plane `plane`: uniform integer in [0, range).
+// int32 ids: 4 draws per Philox block (bits = word q, 32-bit modulo);
+// int64 ids: 2 draws per block (bits = w[2q] | w[2q+1] << 32, 64-bit modulo).
+__device__ __forceinline__ uint64_t philox_draw(PhiloxKey key, uint64_t plane, uint64_t n,
+                                                bool i64, uint64_t range) {
+  const uint64_t per = i64 ? 2 : 4;
+  const uint64_t b = n / per;
+  const uint32_t q = (uint32_t)(n % per);
+  const uint4 w = philox4x32_10(make_uint4((uint32_t)b, (uint32_t)(b >> 32),
+                                           (uint32_t)plane, (uint32_t)(plane >> 32)), key);
+  if (i64) {
+    const uint64_t bits = q == 0 ? ((uint64_t)w.x | ((uint64_t)w.y << 32))
+                                 : ((uint64_t)w.z | ((uint64_t)w.w << 32));
+    return bits % range;
+  }
+  const uint32_t bits = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
+  return (uint64_t)(bits % (uint32_t)range);
+}
+
+// Sampler view shared by the standalone sampler and the fused step.
+struct SamplerView {
+  int32_t kind;
+  bool i64;
+  PhiloxKey key;
+  uint64_t offset;
+  int64_t n_entities;
+  const void* pool;
+  const int32_t* ent_type;
+  const int32_t* type_offsets;
+  const int32_t* type_members;
+  const int32_t* pos_in_type;
+};
+
+__host__ inline SamplerView make_sampler_view(const kge_sampler_desc& s) {
+  SamplerView v;
+  v.kind = s.kind;
+  v.i64 = s.idx_dtype == KGE_IDX_I64;
+  v.key.k0 = (uint32_t)s.seed;
+  v.key.k1 = (uint32_t)(s.seed >> 32);
+  v.offset = s.offset;
+  v.n_entities = s.n_entities;
+  v.pool = s.pool;
+  v.ent_type = s.ent_type;
+  v.type_offsets = s.type_offsets;
+  v.type_members = s.type_members;
+  v.pos_in_type = s.pos_in_type;
+  return v;
+}
+
+__device__ __forceinline__ int64_t load_idx(const void* p, int64_t i, bool i64) {
+  return i64 ? ((const int64_t*)p)[i] : (int64_t)((const int32_t*)p)[i];
+}
+__device__ __forceinline__ void store_idx(void* p, int64_t i, int64_t v, bool i64) {
+  if (i64) ((int64_t*)p)[i] = v; else ((int32_t*)p)[i] = (int32_t)v;
+}
+
+// One negative entity for reference entity `x` (the entity being replaced),
+// draw n of plane `plane`. Returns -1 and sets *err for a singleton type
+// (np.random.choice on an empty pool raises, utils.py:11-16).
+__device__ __forceinline__ int64_t sample_entity(const SamplerView& s, uint64_t plane, uint64_t n,
+                                                 int64_t x, int* err) {
+  if (s.kind == KGE_SAMPLER_UNIFORM) {
+    const uint64_t k = philox_draw(s.key, plane, n, s.i64, (uint64_t)s.n_entities);
+    return s.pool ? load_idx(s.pool, (int64_t)k, s.i64) : (int64_t)k;
+  }
+  // typed: uniform over type2inds[ind2type[x]] minus x (utils.py:12-14)
+  const int32_t ty = s.ent_type[x];
+  const int32_t beg = s.type_offsets[ty], cnt = s.type_offsets[ty + 1] - beg;
+  if (cnt <= 1) { *err = KGE_EINVAL; return -1; }
+  uint64_t k = philox_draw(s.key, plane, n, s.i64, (uint64_t)(cnt - 1));
+  if ((int64_t)k >= s.pos_in_type[x]) ++k;
+  return s.type_members[beg + k];
+}
+
+// ---------------------------------------------------------------- waves
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (KGE_WAVE - 1); }
+__device__ __forceinline__ int wave_id() { return threadIdx.x / KGE_WAVE; }
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, KGE_WAVE);
+  return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, KGE_WAVE));
+  return x;
+}
+
+// ---------------------------------------------------------------- fragments
+template <int VEC, int NC>
+struct Frag {
+  float v[VEC * NC];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) v[i] = 0.f;
+  }
+};
+
+// element index of v[c*VEC + q] on this lane
+template <int VEC>
+__device__ __forceinline__ int frag_elem(int c, int q) { return (c * KGE_WAVE + lane_id()) * VEC + q; }
+
+template <int VEC, int NC>
+__device__ __forceinline__ void load_row(Frag<VEC, NC>& f, const float* __restrict__ row, int cols) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int e0 = (c * KGE_WAVE + lane_id()) * VEC;
+    if (VEC == 4) {
+      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e0 < cols) x = *reinterpret_cast<const float4*>(row + e0);
+      f.v[c * 4 + 0] = x.x; f.v[c * 4 + 1] = x.y; f.v[c * 4 + 2] = x.z; f.v[c * 4 + 3] = x.w;
+    } else if (VEC == 2) {
+      float2 x = make_float2(0.f, 0.f);
+      if (e0 < cols) x = *reinterpret_cast<const float2*>(row + e0);
+      f.v[c * 2 + 0] = x.x; f.v[c * 2 + 1] = x.y;
+    } else {
+      f.v[c] = e0 < cols ? row[e0] : 0.f;
+    }
+  }
+}
+
+template <int VEC, int NC>
+__device__ __forceinline__ void store_row(const Frag<VEC, NC>& f, float* __restrict__ row, int cols) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int e0 = (c * KGE_WAVE + lane_id()) * VEC;
+    if (e0 >= cols) continue;
+    if (VEC == 4) {
+      *reinterpret_cast<float4*>(row + e0) =
+          make_float4(f.v[c * 4 + 0], f.v[c * 4 + 1], f.v[c * 4 + 2], f.v[c * 4 + 3]);
+    } else if (VEC == 2) {
+      *reinterpret_cast<float2*>(row + e0) = make_float2(f.v[c * 2 + 0], f.v[c * 2 + 1]);
+    } else {
+      row[e0] = f.v[c];
+    }
+  }
+}
+
+// Half-width load: element (c*64+l)*VEC/2 + q of a row with cols/2 ... used by
+// RotatE to fetch the phase row so that phase k sits beside complex element k
+// (re, im interleaved in the entity fragment).
+template <int VEC, int NC>
+__device__ __forceinline__ void load_row_half(float (&h)[(VEC / 2 > 0 ? VEC / 2 : 1) * NC],
+                                              const float* __restrict__ row, int cols_half) {
+  constexpr int HV = VEC / 2 > 0 ? VEC / 2 : 1;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int e0 = (c * KGE_WAVE + lane_id()) * HV;
+    if (HV == 2) {
+      float2 x = make_float2(0.f, 0.f);
+      if (e0 < cols_half) x = *reinterpret_cast<const float2*>(row + e0);
+      h[c * 2 + 0] = x.x; h[c * 2 + 1] = x.y;
+    } else {
+      h[c] = e0 < cols_half ? row[e0] : 0.f;
+    }
+  }
+}
+
+template <int VEC, int NC>
+__device__ __forceinline__ void store_row_half(const float (&h)[(VEC / 2 > 0 ? VEC / 2 : 1) * NC],
+                                               float* __restrict__ row, int cols_half) {
+  constexpr int HV = VEC / 2 > 0 ? VEC / 2 : 1;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int e0 = (c * KGE_WAVE + lane_id()) * HV;
+    if (e0 >= cols_half) continue;
+    if (HV == 2) *reinterpret_cast<float2*>(row + e0) = make_float2(h[c * 2 + 0], h[c * 2 + 1]);
+    else row[e0] = h[c];
+  }
+}
+
+__device__ __forceinline__ void set_status(int32_t* status, int code) {
+  if (status) atomicCAS(status, 0, code);
+}
+
+}  // namespace kge

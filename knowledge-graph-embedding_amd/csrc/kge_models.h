@@ -1,0 +1,402 @@
+// Per-model forward / backward policies for the element-wise model family
+// (TransE, DistMult, RotatE). Each policy restates the reference's
+// score_hrt and the TF-2.5 gradient of that op chain, on row fragments
+// (kge_common.h): one wave owns one triple, a lane holds VEC*NC elements.
+//
+// Triple kinds: KIND_POS = the positive (h, r, t); KIND_HC = head-corrupted
+// negative (E replaces h); KIND_TC = tail-corrupted negative (E replaces t)
+// -- the corruption layout of BaseModel.py:360-408.
+//
+// Score element kinds SK (score.py): SK_P1 / SK_P2 / SK_PINF = LpDistance
+// (or LpDistancePow) with p = 1, 2, inf; SK_DOT = Dot.
+#pragma once
+
+#include "kge_common.h"
+
+namespace kge {
+
+enum { KIND_POS = 0, KIND_HC = 1, KIND_TC = 2 };
+enum { SK_P1 = 0, SK_P2 = 1, SK_PINF = 2, SK_DOT = 3 };
+
+constexpr float kPiF = 3.14159265358979323846f;
+
+// ------------------------------------------------------------------ scores
+// Per-lane partial of the score's reduction over the last axis, from
+// a = x - y (Lp kinds) or a = x, b = y (Dot). CPLX: (re, im) interleaved and
+// |.| is the complex modulus (score.py:59-63 on complex64 input).
+template <int SK, bool CPLX, int VEC, int NC>
+__device__ __forceinline__ float score_partial(const Frag<VEC, NC>& a, const Frag<VEC, NC>& b) {
+  float acc = 0.f;
+  if (SK == SK_DOT) {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) acc += a.v[i] * b.v[i];
+    return acc;
+  }
+  if (CPLX) {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; i += 2) {
+      const float m2 = a.v[i] * a.v[i] + a.v[i + 1] * a.v[i + 1];
+      if (SK == SK_P2) acc += m2;
+      else if (SK == SK_P1) acc += sqrtf(m2);
+      else acc = fmaxf(acc, sqrtf(m2));
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) {
+      const float m = fabsf(a.v[i]);
+      if (SK == SK_P2) acc += m * m;
+      else if (SK == SK_P1) acc += m;
+      else acc = fmaxf(acc, m);
+    }
+  }
+  return acc;
+}
+
+// Number of elements attaining the max (for p = inf gradient ties).
+template <bool CPLX, int VEC, int NC>
+__device__ __forceinline__ float tie_partial(const Frag<VEC, NC>& a, float M) {
+  float n = 0.f;
+  if (CPLX) {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; i += 2)
+      n += (sqrtf(a.v[i] * a.v[i] + a.v[i + 1] * a.v[i + 1]) == M) ? 1.f : 0.f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) n += (fabsf(a.v[i]) == M) ? 1.f : 0.f;
+  }
+  return n;
+}
+
+// Scalar score from the reduced value R:
+//   LpDistance:    -pow(clip(R, 1e-9, inf), 1/p); p = inf: -R (max)
+//   LpDistancePow: -(LpDistance)^2
+//   Dot:           R
+template <int SK>
+__device__ __forceinline__ float score_value(float R, bool pw, float* lp_out) {
+  if (SK == SK_DOT) { *lp_out = R; return R; }
+  float lp;
+  if (SK == SK_P2) lp = -sqrtf(fmaxf(R, 1e-9f));
+  else if (SK == SK_P1) lp = -fmaxf(R, 1e-9f);
+  else lp = -R;
+  *lp_out = lp;
+  return pw ? -(lp * lp) : lp;
+}
+
+// dL/ds = c  ->  alpha such that the element gradient is
+//   P2:   g_a = alpha * a                       (TF: pow/clip/sum/pow/abs chain)
+//   P1:   g_a = alpha * sign(a) (complex: a/|a|)
+//   PINF: g_a = alpha * sign(a) on the arg-max set (ties split evenly)
+//   DOT:  g_x = alpha * y, g_y = alpha * x
+template <int SK>
+__device__ __forceinline__ float score_alpha(float c, float R, float lp, float ties, bool pw) {
+  if (SK == SK_DOT) return c;
+  const float clp = pw ? c * (-2.f * lp) : c;   // d(-lp^2)/dlp = -2 lp
+  if (SK == SK_P2) return R >= 1e-9f ? (-clp * 0.5f * rsqrtf(R)) * 2.f : 0.f;
+  if (SK == SK_P1) return R >= 1e-9f ? -clp : 0.f;
+  return -clp / ties;
+}
+
+// Element gradient wrt a (Lp kinds). M = max |a| (PINF only).
+template <int SK, bool CPLX, int VEC, int NC>
+__device__ __forceinline__ void score_grad(const Frag<VEC, NC>& a, float alpha, float M,
+                                           Frag<VEC, NC>& g) {
+  if (SK == SK_P2) {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) g.v[i] = alpha * a.v[i];
+    return;
+  }
+  if (CPLX) {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; i += 2) {
+      const float m = sqrtf(a.v[i] * a.v[i] + a.v[i + 1] * a.v[i + 1]);
+      float s = (m > 0.f) ? alpha / m : 0.f;
+      if (SK == SK_PINF && m != M) s = 0.f;
+      g.v[i] = s * a.v[i];
+      g.v[i + 1] = s * a.v[i + 1];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) {
+      const float x = a.v[i];
+      float s = x > 0.f ? alpha : (x < 0.f ? -alpha : 0.f);
+      if (SK == SK_PINF && fabsf(x) != M) s = 0.f;
+      g.v[i] = s;
+    }
+  }
+}
+
+template <int VEC, int NC>
+__device__ __forceinline__ float sq_partial(const Frag<VEC, NC>& g) {
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VEC * NC; ++i) s += g.v[i] * g.v[i];
+  return s;
+}
+
+template <int VEC, int NC>
+__device__ __forceinline__ void add_to(Frag<VEC, NC>& acc, const Frag<VEC, NC>& g) {
+#pragma unroll
+  for (int i = 0; i < VEC * NC; ++i) acc.v[i] += g.v[i];
+}
+template <int VEC, int NC>
+__device__ __forceinline__ void sub_to(Frag<VEC, NC>& acc, const Frag<VEC, NC>& g) {
+#pragma unroll
+  for (int i = 0; i < VEC * NC; ++i) acc.v[i] -= g.v[i];
+}
+
+// Table view passed to kernels.
+struct TabView {
+  float* p;
+  int64_t ld;
+  int32_t cols;
+  int64_t rows;
+  __device__ __forceinline__ const float* row(int64_t i) const { return p + i * ld; }
+  __device__ __forceinline__ float* row_w(int64_t i) const { return p + i * ld; }
+};
+
+// Model scalars shared by every policy call.
+struct MP {
+  float limit;   // RotatE phase range (RotatE.py:93)
+};
+
+// Snapshot rows written per positive by the score kernel and read back by
+// the update kernel (the positive's context, frozen before any update).
+// All three rows have `snap_cols` floats.
+
+// ======================================================================
+// TransE: s(h + r, t)      (TransE.py:149-155)
+// ======================================================================
+template <int VEC, int NC, int SK>
+struct TransE {
+  static constexpr bool CPLX = false;
+  using F = Frag<VEC, NC>;
+  struct Ctx { F X, R, T; };   // X = h + r
+
+  __device__ static void load_ctx(Ctx& c, const TabView& ent, const TabView& rel, int64_t h,
+                                  int64_t r, int64_t t, const MP&) {
+    F H;
+    load_row(H, ent.row(h), ent.cols);
+    load_row(c.R, rel.row(r), rel.cols);
+    load_row(c.T, ent.row(t), ent.cols);
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) c.X.v[i] = H.v[i] + c.R.v[i];
+  }
+  // a/b for the score (Lp: a = x - y; Dot: a = x, b = y)
+  __device__ static void fwd(const Ctx& c, int kind, const F& E, F& a, F& b) {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) {
+      const float x = kind == KIND_HC ? E.v[i] + c.R.v[i] : c.X.v[i];
+      const float y = kind == KIND_TC ? E.v[i] : c.T.v[i];
+      if (SK == SK_DOT) { a.v[i] = x; b.v[i] = y; }
+      else a.v[i] = x - y;
+    }
+  }
+  // gradients wrt x and y from a/b
+  __device__ static void grad_xy(const F& a, const F& b, float alpha, float M, F& gx, F& gy) {
+    if (SK == SK_DOT) {
+#pragma unroll
+      for (int i = 0; i < VEC * NC; ++i) { gx.v[i] = alpha * b.v[i]; gy.v[i] = alpha * a.v[i]; }
+    } else {
+      score_grad<SK, false>(a, alpha, M, gx);
+#pragma unroll
+      for (int i = 0; i < VEC * NC; ++i) gy.v[i] = -gx.v[i];
+    }
+  }
+  // accumulate the fixed rows (H: accH, R: accR, T: accT) and the per-variable
+  // sum of squared IndexedSlices values (norm[0] ent_emb, norm[1] rel_emb).
+  __device__ static void bwd(const Ctx& c, int kind, const F& E, const F& a, const F& b,
+                             float alpha, float M, F& accH, F& accR, F& accT, float* nrm,
+                             const MP&) {
+    F gx, gy;
+    grad_xy(a, b, alpha, M, gx, gy);
+    const float sx = sq_partial(gx), sy = sq_partial(gy);
+    nrm[0] += sx + sy;   // h-lookup slice + t-lookup slice
+    nrm[1] += sx;        // r-lookup slice
+    add_to(accR, gx);
+    if (kind != KIND_HC) add_to(accH, gx);
+    if (kind != KIND_TC) add_to(accT, gy);
+  }
+  __device__ static void write_snap(const Ctx& c, float* s0, float* s1, float* s2, int cols) {
+    store_row(c.X, s0, cols);
+    store_row(c.R, s1, cols);
+    store_row(c.T, s2, cols);
+  }
+  // update-kernel side: gradient of a negative wrt its sampled entity row E
+  __device__ static void grad_entity(const float* s0, const float* s1, const float* s2, int cols,
+                                     int kind, const F& E, float alpha, float M, F& gE) {
+    Ctx c;
+    if (kind == KIND_TC) load_row(c.X, s0, cols);
+    else { load_row(c.R, s1, cols); load_row(c.T, s2, cols); }
+    F a, b, gx, gy;
+    fwd(c, kind, E, a, b);
+    grad_xy(a, b, alpha, M, gx, gy);
+    gE = kind == KIND_HC ? gx : gy;
+  }
+};
+
+// ======================================================================
+// DistMult: sum(h * r * t)     (DistMult.py:140-146); score_fn not used
+// ======================================================================
+template <int VEC, int NC, int SK_UNUSED>
+struct DistMult {
+  static constexpr bool CPLX = false;
+  using F = Frag<VEC, NC>;
+  struct Ctx { F H, R, T, HR; };
+
+  __device__ static void load_ctx(Ctx& c, const TabView& ent, const TabView& rel, int64_t h,
+                                  int64_t r, int64_t t, const MP&) {
+    load_row(c.H, ent.row(h), ent.cols);
+    load_row(c.R, rel.row(r), rel.cols);
+    load_row(c.T, ent.row(t), ent.cols);
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) c.HR.v[i] = c.H.v[i] * c.R.v[i];
+  }
+  // a = h*r, b = t   (TF evaluates (h * r) * t)
+  __device__ static void fwd(const Ctx& c, int kind, const F& E, F& a, F& b) {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) {
+      a.v[i] = kind == KIND_HC ? E.v[i] * c.R.v[i] : c.HR.v[i];
+      b.v[i] = kind == KIND_TC ? E.v[i] : c.T.v[i];
+    }
+  }
+  __device__ static void bwd(const Ctx& c, int kind, const F& E, const F& a, const F& b,
+                             float alpha, float M, F& accH, F& accR, F& accT, float* nrm,
+                             const MP&) {
+    F gH, gR, gT;
+    const F& Hv = kind == KIND_HC ? E : c.H;
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) {
+      const float ga = alpha * b.v[i];   // d/d(h*r)
+      gT.v[i] = alpha * a.v[i];
+      gH.v[i] = ga * c.R.v[i];
+      gR.v[i] = ga * Hv.v[i];
+    }
+    nrm[0] += sq_partial(gH) + sq_partial(gT);
+    nrm[1] += sq_partial(gR);
+    add_to(accR, gR);
+    if (kind != KIND_HC) add_to(accH, gH);
+    if (kind != KIND_TC) add_to(accT, gT);
+  }
+  __device__ static void write_snap(const Ctx& c, float* s0, float* s1, float* s2, int cols) {
+    store_row(c.HR, s0, cols);
+    store_row(c.R, s1, cols);
+    store_row(c.T, s2, cols);
+  }
+  __device__ static void grad_entity(const float* s0, const float* s1, const float* s2, int cols,
+                                     int kind, const F& E, float alpha, float M, F& gE) {
+    if (kind == KIND_TC) {   // d/dt = c * (h*r)
+      F HR;
+      load_row(HR, s0, cols);
+#pragma unroll
+      for (int i = 0; i < VEC * NC; ++i) gE.v[i] = alpha * HR.v[i];
+    } else {                 // d/dh = (c * t) * r
+      F R, T;
+      load_row(R, s1, cols);
+      load_row(T, s2, cols);
+#pragma unroll
+      for (int i = 0; i < VEC * NC; ++i) gE.v[i] = (alpha * T.v[i]) * R.v[i];
+    }
+  }
+};
+
+// ======================================================================
+// RotatE: s(h o e^{i theta}, t), theta = r / limit * pi   (RotatE.py:148-165)
+// ent rows are [d, 2] (re, im interleaved) -> 2d floats; rel rows d phases.
+// VEC must be 2 or 4 (complex pairs stay inside one lane).
+// ======================================================================
+template <int VEC, int NC, int SK>
+struct RotatE {
+  static constexpr bool CPLX = true;
+  static constexpr int HV = VEC / 2;
+  using F = Frag<VEC, NC>;
+  struct Ctx { F H, X, CS, T; };   // CS = (cos, sin) interleaved, X = H o CS
+  __device__ static void load_ctx(Ctx& c, const TabView& ent, const TabView& rel, int64_t h,
+                                  int64_t r, int64_t t, const MP& mp) {
+    const float limit = mp.limit;
+    load_row(c.H, ent.row(h), ent.cols);
+    load_row(c.T, ent.row(t), ent.cols);
+    float ph[HV * NC];
+    load_row_half<VEC, NC>(ph, rel.row(r), rel.cols);
+#pragma unroll
+    for (int k = 0; k < HV * NC; ++k) {
+      const float th = (ph[k] / limit) * kPiF;
+      c.CS.v[2 * k] = cosf(th);
+      c.CS.v[2 * k + 1] = sinf(th);
+    }
+    cmul(c.H, c.CS, c.X);
+  }
+  __device__ static void cmul(const F& A, const F& W, F& out) {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; i += 2) {
+      out.v[i] = A.v[i] * W.v[i] - A.v[i + 1] * W.v[i + 1];
+      out.v[i + 1] = A.v[i] * W.v[i + 1] + A.v[i + 1] * W.v[i];
+    }
+  }
+  __device__ static void fwd(const Ctx& c, int kind, const F& E, F& a, F& b) {
+    F x;
+    if (kind == KIND_HC) cmul(E, c.CS, x); else x = c.X;
+    const F& y = kind == KIND_TC ? E : c.T;
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) a.v[i] = x.v[i] - y.v[i];
+  }
+  // g_h = g_x * conj(w); g_theta = gxi * x_re - gxr * x_im
+  __device__ static void bwd(const Ctx& c, int kind, const F& E, const F& a, const F& b,
+                             float alpha, float M, F& accH, F& accR, F& accT, float* nrm,
+                             const MP& mp) {
+    const float limit = mp.limit;
+    F gx;
+    score_grad<SK, true>(a, alpha, M, gx);
+    F x;
+    if (kind == KIND_HC) cmul(E, c.CS, x); else x = c.X;
+    F gH;
+    float gth2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VEC * NC; i += 2) {
+      const float co = c.CS.v[i], si = c.CS.v[i + 1];
+      gH.v[i] = gx.v[i] * co + gx.v[i + 1] * si;
+      gH.v[i + 1] = gx.v[i + 1] * co - gx.v[i] * si;
+      const float gth = gx.v[i + 1] * x.v[i] - gx.v[i] * x.v[i + 1];
+      const float gr = (gth * kPiF) / limit;
+      accR.v[i] += gr;   // phase gradient kept in the even slot
+      gth2 += gr * gr;
+    }
+    const float sx = sq_partial(gH), sy = sq_partial(gx);   // |g_t| = |g_u|
+    nrm[0] += sx + sy;
+    nrm[1] += gth2;
+    if (kind != KIND_HC) add_to(accH, gH);
+    if (kind != KIND_TC) sub_to(accT, gx);
+  }
+  __device__ static void write_snap(const Ctx& c, float* s0, float* s1, float* s2, int cols) {
+    store_row(c.X, s0, cols);
+    store_row(c.CS, s1, cols);
+    store_row(c.T, s2, cols);
+  }
+  __device__ static void grad_entity(const float* s0, const float* s1, const float* s2, int cols,
+                                     int kind, const F& E, float alpha, float M, F& gE) {
+    if (kind == KIND_TC) {
+      F X, a, g;
+      load_row(X, s0, cols);
+#pragma unroll
+      for (int i = 0; i < VEC * NC; ++i) a.v[i] = X.v[i] - E.v[i];
+      score_grad<SK, true>(a, alpha, M, g);
+#pragma unroll
+      for (int i = 0; i < VEC * NC; ++i) gE.v[i] = -g.v[i];
+    } else {
+      F CS, T, x, a, g;
+      load_row(CS, s1, cols);
+      load_row(T, s2, cols);
+      cmul(E, CS, x);
+#pragma unroll
+      for (int i = 0; i < VEC * NC; ++i) a.v[i] = x.v[i] - T.v[i];
+      score_grad<SK, true>(a, alpha, M, g);
+#pragma unroll
+      for (int i = 0; i < VEC * NC; i += 2) {
+        const float co = CS.v[i], si = CS.v[i + 1];
+        gE.v[i] = g.v[i] * co + g.v[i + 1] * si;
+        gE.v[i + 1] = g.v[i + 1] * co - g.v[i] * si;
+      }
+    }
+  }
+};
+
+}  // namespace kge

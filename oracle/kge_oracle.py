@@ -1,0 +1,350 @@
+"""CPU oracle for the KGE training step -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this module, and only as the checker (or the
+timed CPU baseline); the product (``KGE``) never does.
+
+What it restates (reference = melissakou/knowledge-graph-embedding, TF 2.5):
+  * negative draws: the counter-based spec of ``include/kge_hip.h``
+    (Philox4x32-10, pinned by the Random123 known-answer vectors in
+    ``tests/golden/philox_kat.json``) in the corruption layout of
+    ``BaseModel.py:332-408`` (h-side draws, then t-side; 'h+t' rows
+    alternate h-corrupt / t-corrupt per positive);
+  * typed draws: ``utils.py:11-16`` (pool of the entity's type minus the
+    entity) mapped from the same counter stream;
+  * the step ``BaseModel.py:316-328``: constraint assigns, scores
+    (``score.py:49-89`` per model ``score_hrt``), loss (``loss.py``), TF-2.5
+    gradients with embedding lookups as IndexedSlices (values of every
+    lookup kept, duplicates NOT summed; any dense contribution turns the
+    variable's gradient dense -- ``backprop.aggregate_indexed_slices_gradients``),
+    ``clip_by_norm(g, 5)`` per variable (``values * 5 / max(||values||, 5)``),
+    keras SGD (``ResourceScatterAdd(var, idx, -lr * g)``).
+  Arithmetic is float64 torch autograd on the op sequence the reference
+  writes (each op's TF gradient rule coincides with torch's: clip passes on
+  the closed interval, abs'(0) = 0, |z|'(0) = 0, reduce_max splits ties).
+
+PARITY UNPINNED: the reference's own tests pin only properties (shape, sign,
+finiteness), TF 2.5 is not installed and cannot be imported here, and the
+reference's negatives are unseeded (irreproducible). The restatement is
+cross-checked against finite differences and the reference's property tests
+(``tests/test_oracle.py``); golden vectors under ``tests/golden`` are
+generated from it by ``tests/golden/make_golden.py``.
+"""
+
+import math
+
+import numpy as np
+import torch
+
+F64 = torch.float64
+
+# ---------------------------------------------------------------- Philox
+_M0, _M1 = 0xD2511F53, 0xCD9E8D57
+_W0, _W1 = 0x9E3779B9, 0xBB67AE85
+
+
+def philox4x32_10(ctr, key):
+    """Scalar reference Philox4x32-10 (Salmon et al. 2011; Random123)."""
+    c = [int(x) & 0xFFFFFFFF for x in ctr]
+    k0, k1 = int(key[0]) & 0xFFFFFFFF, int(key[1]) & 0xFFFFFFFF
+    for r in range(10):
+        if r:
+            k0 = (k0 + _W0) & 0xFFFFFFFF
+            k1 = (k1 + _W1) & 0xFFFFFFFF
+        p0 = _M0 * c[0]
+        p1 = _M1 * c[2]
+        c = [((p1 >> 32) ^ c[1] ^ k0) & 0xFFFFFFFF, p1 & 0xFFFFFFFF,
+             ((p0 >> 32) ^ c[3] ^ k1) & 0xFFFFFFFF, p0 & 0xFFFFFFFF]
+    return c
+
+
+def _philox_vec(b, plane, seed):
+    """Vectorised over block indices b (numpy uint64)."""
+    b = np.asarray(b, dtype=np.uint64)
+    m = np.uint64(0xFFFFFFFF)
+    c = [b & m, b >> np.uint64(32), np.full_like(b, plane & 0xFFFFFFFF), np.full_like(b, (plane >> 32) & 0xFFFFFFFF)]
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    for r in range(10):
+        if r:
+            k0 = (k0 + _W0) & 0xFFFFFFFF
+            k1 = (k1 + _W1) & 0xFFFFFFFF
+        p0 = np.uint64(_M0) * c[0]
+        p1 = np.uint64(_M1) * c[2]
+        c = [(p1 >> np.uint64(32)) ^ c[1] ^ np.uint64(k0), p1 & m, (p0 >> np.uint64(32)) ^ c[3] ^ np.uint64(k1), p0 & m]
+    return np.stack(c, axis=-1)
+
+
+def draw_bits(seed, plane, n, i64):
+    """Raw bits of draw indices n: u32 word n%4 of block n//4 (int32 ids), or
+    w[2q] | w[2q+1] << 32 of block n//2 (int64 ids)."""
+    n = np.asarray(n, dtype=np.uint64)
+    if i64:
+        w = _philox_vec(n // np.uint64(2), plane, seed)
+        q = (n % np.uint64(2)).astype(np.int64)
+        lo = w[np.arange(len(n)), 2 * q]
+        hi = w[np.arange(len(n)), 2 * q + 1]
+        return lo | (hi << np.uint64(32))
+    w = _philox_vec(n // np.uint64(4), plane, seed)
+    return w[np.arange(len(n)), (n % np.uint64(4)).astype(np.int64)]
+
+
+def _side_draws(ref_ent, k, seed, plane, i64, sampler, E, typed=None):
+    """k draws per positive for one side (ns_strategy.py:57-62 / utils.py:11-16)."""
+    B = len(ref_ent)
+    n = np.arange(B * k)
+    bits = draw_bits(seed, plane, n, i64)
+    if sampler == "uniform":
+        return (bits % np.uint64(E)).astype(np.int64)
+    ent_type, offsets, members, pos_in_type = typed
+    x = np.repeat(np.asarray(ref_ent, dtype=np.int64), k)
+    ty = ent_type[x]
+    beg, cnt = offsets[ty], offsets[ty + 1] - offsets[ty]
+    assert (cnt > 1).all(), "empty typed pool"
+    kk = (bits % (cnt - 1).astype(np.uint64)).astype(np.int64)
+    kk = kk + (kk >= pos_in_type[x])
+    return members[beg + kk].astype(np.int64)
+
+
+def negatives(pos, K, side, E, seed, plane, i64=True, sampler="uniform", typed=None):
+    """Negative entity ids in the reference layout, [B * K_eff]."""
+    pos = np.asarray(pos, dtype=np.int64)
+    if side == "h":
+        return _side_draws(pos[:, 0], K, seed, plane, i64, sampler, E, typed)
+    if side == "t":
+        return _side_draws(pos[:, 2], K, seed, plane, i64, sampler, E, typed)
+    k = K // 2
+    hs = _side_draws(pos[:, 0], k, seed, plane, i64, sampler, E, typed).reshape(-1, k)
+    ts = _side_draws(pos[:, 2], k, seed, plane + 1, i64, sampler, E, typed).reshape(-1, k)
+    return np.stack([hs, ts], axis=-1).reshape(-1)   # alternate h, t per slot
+
+
+def uniform_negatives(pos, K, side, E, seed, plane, i64=True):
+    return negatives(pos, K, side, E, seed, plane, i64)
+
+
+def typed_tables(ind2type):
+    """CSR form of type2inds built as BaseModel.py:258-263 does."""
+    ind2type = list(ind2type)
+    types = list(np.unique(ind2type))
+    tid = {t: i for i, t in enumerate(types)}
+    members, offsets = [], [0]
+    pos_in = np.zeros(len(ind2type), np.int64)
+    for t in types:
+        inds = [i for (i, ti) in enumerate(ind2type) if ti == t]
+        for k, e in enumerate(inds):
+            pos_in[e] = k
+        members += inds
+        offsets.append(len(members))
+    return (np.array([tid[t] for t in ind2type], np.int64), np.array(offsets, np.int64),
+            np.array(members, np.int64), pos_in)
+
+
+def corrupt(pos, neg_ids, K, side):
+    """[B*K_eff, 3] negative triples (BaseModel.py:360-408)."""
+    pos = np.asarray(pos, dtype=np.int64)
+    Keff = 2 * (K // 2) if side == "h+t" else K
+    rep = np.repeat(pos, Keff, axis=0).copy()
+    neg_ids = np.asarray(neg_ids, dtype=np.int64)
+    if side == "h":
+        rep[:, 0] = neg_ids
+    elif side == "t":
+        rep[:, 2] = neg_ids
+    else:
+        j = np.tile(np.arange(Keff), len(pos))
+        hmask = (j % 2) == 0
+        rep[hmask, 0] = neg_ids[hmask]
+        rep[~hmask, 2] = neg_ids[~hmask]
+    return rep
+
+
+# ---------------------------------------------------------------- scores / losses
+def score_fn(kind, p, x, y):
+    """score.py:49-89."""
+    if kind == "dot":
+        return torch.sum(x * y, dim=-1)
+    diff = torch.abs(x - y)
+    if math.isinf(p):
+        lp = -torch.amax(diff, dim=-1)
+    else:
+        lp = -torch.pow(torch.clamp(torch.sum(torch.pow(diff, p), dim=-1), min=1e-9), 1.0 / p)
+    if kind == "lp":
+        return lp
+    return -torch.pow(lp, 2)
+
+
+def loss_fn(spec, pos, neg, batch_scale=1.0):
+    """loss.py:49-204; spec = ('hinge', m) | ('logistic',) | ('bce',) | ('sans', m, T) | ('sqerr',)."""
+    name = spec[0]
+    B = pos.shape[0]
+    K = int(neg.shape[0] / B)
+    Bg = B * batch_scale
+    if name == "hinge":
+        p = torch.repeat_interleave(pos, K)
+        return torch.sum(torch.clamp(spec[1] + neg - p, min=0)) / (p.shape[0] * batch_scale)
+    if name == "logistic":
+        p = torch.repeat_interleave(pos, K)
+        return torch.sum(torch.log(1 + torch.exp(neg - p)))
+    if name == "bce":
+        return -(torch.sum(torch.nn.functional.logsigmoid(pos)) + torch.sum(torch.nn.functional.logsigmoid(-neg))) / Bg
+    if name == "sans":
+        m, T = spec[1], spec[2]
+        n = neg.reshape(B, K)
+        prob = torch.softmax(T * n, dim=-1).detach()
+        return -(torch.sum(torch.nn.functional.logsigmoid(pos + m)) +
+                 torch.sum(prob * torch.nn.functional.logsigmoid(-n - m))) / Bg
+    if name == "sqerr":
+        return (torch.sum((pos - 1.0) ** 2) + torch.sum(neg ** 2)) / 2 / Bg
+    raise ValueError(name)
+
+
+def _norm_rows(X, axis):
+    return X / torch.pow(torch.sum(torch.abs(X) ** 2, dim=axis, keepdim=True), 0.5)
+
+
+def _clip_rows(X):
+    n = torch.pow(torch.sum(torch.abs(X) ** 2, dim=-1, keepdim=True), 0.5)
+    mask = (n < 1).to(X.dtype)
+    return mask * X + (1 - mask) * (X / torch.clamp(n, min=1e-9) * 1)
+
+
+# ---------------------------------------------------------------- models
+class _Lookups:
+    def __init__(self, W, train):
+        self.W, self.train, self.rec = W, train, []
+
+    def __call__(self, name, idx):
+        idx = torch.as_tensor(idx, dtype=torch.int64)
+        if not self.train:
+            return self.W[name][idx]
+        leaf = self.W[name].detach()[idx.reshape(-1)].clone().requires_grad_(True)
+        self.rec.append((name, idx.reshape(-1), leaf))
+        return leaf.reshape(tuple(idx.shape) + tuple(self.W[name].shape[1:]))
+
+
+def _score_hrt(model, W, L, h, r, t, score, cfg):
+    kind, p = score
+    if model == "TransE":
+        return score_fn(kind, p, L("ent_emb", h) + L("rel_emb", r), L("ent_emb", t))
+    if model == "DistMult":
+        return torch.sum(L("ent_emb", h) * L("rel_inter", r) * L("ent_emb", t), dim=-1)
+    if model == "RotatE":
+        he, re_, te = L("ent_emb", h), L("rel_emb", r), L("ent_emb", t)
+        th = re_ / cfg["limit"] * np.float32(np.pi).item()
+        x = torch.complex(he[..., 0], he[..., 1]) * torch.complex(torch.cos(th), torch.sin(th))
+        return score_fn(kind, p, x, torch.complex(te[..., 0], te[..., 1]))
+    if model == "TransH":
+        he, re_, w, te = L("ent_emb", h), L("rel_emb", r), L("rel_hyper", r), L("ent_emb", t)
+        hp = he - torch.sum(w * he, -1, keepdim=True) * w
+        tp = te - torch.sum(w * te, -1, keepdim=True) * w
+        return score_fn(kind, p, hp + re_, tp)
+    if model == "TransR":
+        he, re_, te, M = L("ent_emb", h), L("rel_emb", r), L("ent_emb", t), L("rel_proj", r)
+        hp = torch.matmul(he.unsqueeze(-2), M).squeeze(-2)
+        tp = torch.matmul(te.unsqueeze(-2), M).squeeze(-2)
+        if cfg["constraint"]:
+            hp, tp = _clip_rows(hp), _clip_rows(tp)
+        return score_fn(kind, p, hp + re_, tp)
+    if model == "TransD":
+        he, re_, te = L("ent_emb", h), L("rel_emb", r), L("ent_emb", t)
+        hpj, rpj, tpj = L("ent_proj", h), L("rel_proj", r), L("ent_proj", t)
+        kr, ke = re_.shape[-1], he.shape[-1]
+        eye = torch.eye(kr, ke, dtype=he.dtype)
+        hm = torch.matmul(rpj.unsqueeze(-1), hpj.unsqueeze(-2)) + eye
+        tm = torch.matmul(rpj.unsqueeze(-1), tpj.unsqueeze(-2)) + eye
+        hp = torch.matmul(hm, he.unsqueeze(-1)).squeeze(-1)
+        tp = torch.matmul(tm, te.unsqueeze(-1)).squeeze(-1)
+        if cfg["constraint"]:
+            hp, tp = _clip_rows(hp), _clip_rows(tp)
+        return score_fn(kind, p, hp + re_, tp)
+    if model == "RESCAL":
+        he, te, Rm = L("ent_emb", h), L("ent_emb", t), L("rel_inter", r)
+        return torch.matmul(torch.matmul(he.unsqueeze(-2), Rm), te.unsqueeze(-1)).reshape(-1)
+    raise ValueError(model)
+
+
+def _constraint(model, W, L, X, cfg, batch_scale):
+    """Per-model _constraint_loss: assigns (no grad) + returned term."""
+    if not cfg["constraint"]:
+        return 0.0
+    lam = cfg.get("constraint_weight", 1.0)
+    with torch.no_grad():
+        if model in ("TransE", "DistMult"):
+            W["ent_emb"].copy_(_norm_rows(W["ent_emb"], 1))
+        if model in ("TransR", "TransD"):
+            W["ent_emb"].copy_(_clip_rows(W["ent_emb"]))
+            W["rel_emb"].copy_(_clip_rows(W["rel_emb"]))
+        if model == "TransH":
+            W["rel_hyper"].copy_(_norm_rows(W["rel_hyper"], 1))
+    if model == "DistMult":
+        r = L("rel_inter", X[:, 1])
+        reg = torch.sum(torch.abs(r) ** 2, dim=-1)
+        return lam * torch.sum(reg) / (reg.shape[0] * batch_scale)
+    if model == "TransH":
+        e = W["ent_emb"]
+        norm = torch.pow(torch.sum(torch.abs(e) ** 2, -1, keepdim=True), 0.5)
+        scale = torch.sum(torch.clamp(norm ** 2 - 1, min=0))
+        orth = torch.sum(W["rel_hyper"] * W["rel_emb"], -1)
+        orth = torch.pow(orth / torch.linalg.norm(W["rel_emb"], dim=-1), 2) - 1e-18
+        return lam * (scale + torch.sum(torch.clamp(orth, min=0)))
+    if model == "RESCAL":
+        e_norm = torch.mean(torch.sum(torch.abs(W["ent_emb"]) ** 2, -1))
+        r_norm = torch.mean(torch.sum(torch.abs(W["rel_inter"]) ** 2, dim=(1, 2)))
+        return lam * (e_norm + r_norm)
+    return 0.0
+
+
+def train_step(model, weights, pos, neg_ids, score=("lp", 2.0), loss=("hinge", 1.0), lr=0.01, constraint=True,
+               constraint_weight=1.0, side="h+t", train=True, batch_scale=1.0, limit=None,
+               clip_norm=5.0):
+    """One reference step with injected negatives. Returns dict with loss,
+    pos_score, neg_score, weights (numpy, updated) and norm2 per variable."""
+    W = {k: torch.tensor(np.asarray(v), dtype=F64) for k, v in weights.items()}
+    names = list(W.keys())
+    pos = np.asarray(pos, dtype=np.int64)
+    B = len(pos)
+    Keff = len(neg_ids) // max(B, 1)
+    negt = corrupt(pos, neg_ids, Keff, side)
+    cfg = {"constraint": constraint, "constraint_weight": constraint_weight, "limit": limit}
+    L = _Lookups(W, train)
+    if train:
+        for w in W.values():
+            w.requires_grad_(True)
+    with torch.set_grad_enabled(train):
+        cterm = _constraint(model, W, L, torch.as_tensor(pos), cfg, batch_scale)
+        ps = _score_hrt(model, W, L, pos[:, 0], pos[:, 1], pos[:, 2], score, cfg)
+        ns = _score_hrt(model, W, L, negt[:, 0], negt[:, 1], negt[:, 2], score, cfg)
+        lval = loss_fn(loss, ps, ns, batch_scale) + cterm
+    out = {"loss": float(lval), "pos_score": ps.detach().numpy(), "neg_score": ns.detach().numpy(),
+           "norm2": {}}
+    if train:
+        leaves = [x[2] for x in L.rec]
+        grads = torch.autograd.grad(lval, [W[n] for n in names] + leaves, allow_unused=True)
+        dense = dict(zip(names, grads[:len(names)]))
+        slices = {}
+        for (n, idx, _), g in zip(L.rec, grads[len(names):]):
+            if g is not None:
+                slices.setdefault(n, []).append((idx, g))
+        with torch.no_grad():
+            for n in names:
+                w = W[n]
+                w.requires_grad_(False)
+                dg, sl = dense.get(n), slices.get(n, [])
+                if dg is None and not sl:
+                    continue
+                if dg is not None:
+                    tot = dg.clone()
+                    for idx, g in sl:
+                        tot.index_add_(0, idx, g)
+                    l2 = torch.sum(tot * tot)
+                    out["norm2"][n] = float(l2)
+                    tot = tot * clip_norm / max(math.sqrt(float(l2)), clip_norm)
+                    w.add_(-lr * tot)
+                else:
+                    idx = torch.cat([i for i, _ in sl])
+                    vals = torch.cat([g for _, g in sl])
+                    l2 = torch.sum(vals * vals)
+                    out["norm2"][n] = float(l2)
+                    vals = vals * clip_norm / max(math.sqrt(float(l2)), clip_norm)
+                    w.index_add_(0, idx, -lr * vals)
+    out["weights"] = {k: v.detach().numpy() for k, v in W.items()}
+    return out
