@@ -20,6 +20,13 @@ enum { SK_P1 = 0, SK_P2 = 1, SK_PINF = 2, SK_DOT = 3 };
 
 constexpr float kPiF = 3.14159265358979323846f;
 
+// |z| of a complex element, evaluated identically at every call site (no
+// contraction differences), so the p = inf arg-max test is exact.
+__device__ __forceinline__ float cmod(float re, float im) {
+#pragma clang fp contract(off)
+  return sqrtf(re * re + im * im);
+}
+
 // ------------------------------------------------------------------ scores
 // Per-lane partial of the score's reduction over the last axis, from
 // a = x - y (Lp kinds) or a = x, b = y (Dot). CPLX: (re, im) interleaved and
@@ -35,10 +42,9 @@ __device__ __forceinline__ float score_partial(const Frag<VEC, NC>& a, const Fra
   if (CPLX) {
 #pragma unroll
     for (int i = 0; i < VEC * NC; i += 2) {
-      const float m2 = a.v[i] * a.v[i] + a.v[i + 1] * a.v[i + 1];
-      if (SK == SK_P2) acc += m2;
-      else if (SK == SK_P1) acc += sqrtf(m2);
-      else acc = fmaxf(acc, sqrtf(m2));
+      if (SK == SK_P2) acc += a.v[i] * a.v[i] + a.v[i + 1] * a.v[i + 1];
+      else if (SK == SK_P1) acc += cmod(a.v[i], a.v[i + 1]);
+      else acc = fmaxf(acc, cmod(a.v[i], a.v[i + 1]));
     }
   } else {
 #pragma unroll
@@ -59,7 +65,7 @@ __device__ __forceinline__ float tie_partial(const Frag<VEC, NC>& a, float M) {
   if (CPLX) {
 #pragma unroll
     for (int i = 0; i < VEC * NC; i += 2)
-      n += (sqrtf(a.v[i] * a.v[i] + a.v[i + 1] * a.v[i + 1]) == M) ? 1.f : 0.f;
+      n += (cmod(a.v[i], a.v[i + 1]) == M) ? 1.f : 0.f;
   } else {
 #pragma unroll
     for (int i = 0; i < VEC * NC; ++i) n += (fabsf(a.v[i]) == M) ? 1.f : 0.f;
@@ -108,7 +114,7 @@ __device__ __forceinline__ void score_grad(const Frag<VEC, NC>& a, float alpha, 
   if (CPLX) {
 #pragma unroll
     for (int i = 0; i < VEC * NC; i += 2) {
-      const float m = sqrtf(a.v[i] * a.v[i] + a.v[i + 1] * a.v[i + 1]);
+      const float m = cmod(a.v[i], a.v[i + 1]);
       float s = (m > 0.f) ? alpha / m : 0.f;
       if (SK == SK_PINF && m != M) s = 0.f;
       g.v[i] = s * a.v[i];
@@ -325,7 +331,10 @@ struct RotatE {
     }
     cmul(c.H, c.CS, c.X);
   }
+  // complex product, rounded op by op (no contraction): the update kernel
+  // re-derives it and must get the same bits as the score kernel did
   __device__ static void cmul(const F& A, const F& W, F& out) {
+#pragma clang fp contract(off)
 #pragma unroll
     for (int i = 0; i < VEC * NC; i += 2) {
       out.v[i] = A.v[i] * W.v[i] - A.v[i + 1] * W.v[i + 1];

@@ -410,6 +410,32 @@ __global__ __launch_bounds__(256) void score_kernel(StepArgs A) {
   }
 }
 
+// relation-row fragments: full layout, or RotatE's half layout
+template <bool HALF, int VEC, int NC>
+__device__ __forceinline__ void load_rel_row(float (&v)[(HALF ? (VEC / 2 > 0 ? VEC / 2 : 1) : VEC) * NC],
+                                             const float* row, int cols) {
+  if constexpr (HALF) {
+    load_row_half<VEC, NC>(v, row, cols);
+  } else {
+    Frag<VEC, NC> f;
+    load_row(f, row, cols);
+#pragma unroll
+    for (int q = 0; q < VEC * NC; ++q) v[q] = f.v[q];
+  }
+}
+template <bool HALF, int VEC, int NC>
+__device__ __forceinline__ void store_rel_row(const float (&v)[(HALF ? (VEC / 2 > 0 ? VEC / 2 : 1) : VEC) * NC],
+                                              float* row, int cols) {
+  if constexpr (HALF) {
+    store_row_half<VEC, NC>(v, row, cols);
+  } else {
+    Frag<VEC, NC> f;
+#pragma unroll
+    for (int q = 0; q < VEC * NC; ++q) f.v[q] = v[q];
+    store_row(f, row, cols);
+  }
+}
+
 // ------------------------------------------------------------ KU update
 // blocks [0, P): entity buckets; [P, P + Pr): relation groups (one wave per
 // relation). Block 0 also reduces the loss.
@@ -457,8 +483,11 @@ __global__ __launch_bounds__(256) void update_kernel(StepArgs A) {
     // ---------------- relation rows: one wave per relation, positives in order
     const int64_t r = (int64_t)(blockIdx.x - A.P) * W + wv;
     if (r >= A.rel.rows) return;
-    F acc;
-    acc.zero();
+    // RotatE phase rows use the half-width layout (phase k beside complex k)
+    constexpr int RV = M::CPLX ? (VEC / 2 > 0 ? VEC / 2 : 1) : VEC;
+    float acc[RV * NC];
+#pragma unroll
+    for (int q = 0; q < RV * NC; ++q) acc[q] = 0.f;
     bool any = false;
     for (int64_t i0 = 0; i0 < A.B; i0 += KGE_WAVE) {
       const int64_t i = i0 + lane;
@@ -468,19 +497,21 @@ __global__ __launch_bounds__(256) void update_kernel(StepArgs A) {
       while (bal) {
         const int l = __ffsll((long long)bal) - 1;
         bal &= bal - 1;
-        F g;
-        load_row(g, A.gpos + (i0 + l) * 3 * (int64_t)A.gcols + A.gcols, A.rel_gcols);
-        add_to(acc, g);
+        const float* g = A.gpos + (i0 + l) * 3 * (int64_t)A.gcols + A.gcols;
+        float gv[RV * NC];
+        load_rel_row<M::CPLX, VEC, NC>(gv, g, A.rel_gcols);
+#pragma unroll
+        for (int q = 0; q < RV * NC; ++q) acc[q] += gv[q];
         any = true;
       }
     }
     if (!any) return;
-    F row;
-    load_row(row, A.rel.row(r), A.rel.cols);
+    float row[RV * NC];
+    load_rel_row<M::CPLX, VEC, NC>(row, A.rel.row(r), A.rel.cols);
     const float sc = s_scale[1];
 #pragma unroll
-    for (int q = 0; q < VEC * NC; ++q) row.v[q] = row.v[q] + acc.v[q] * sc;
-    store_row(row, A.rel.row_w(r), A.rel.cols);
+    for (int q = 0; q < RV * NC; ++q) row[q] = row[q] + acc[q] * sc;
+    store_rel_row<M::CPLX, VEC, NC>(row, A.rel.row_w(r), A.rel.cols);
     return;
   }
 

@@ -113,8 +113,9 @@ def negatives(pos, K, side, E, seed, plane, i64=True, sampler="uniform", typed=N
     if side == "t":
         return _side_draws(pos[:, 2], K, seed, plane, i64, sampler, E, typed)
     k = K // 2
-    hs = _side_draws(pos[:, 0], k, seed, plane, i64, sampler, E, typed).reshape(-1, k)
-    ts = _side_draws(pos[:, 2], k, seed, plane + 1, i64, sampler, E, typed).reshape(-1, k)
+    B = len(pos)
+    hs = _side_draws(pos[:, 0], k, seed, plane, i64, sampler, E, typed).reshape(B, k)
+    ts = _side_draws(pos[:, 2], k, seed, plane + 1, i64, sampler, E, typed).reshape(B, k)
     return np.stack([hs, ts], axis=-1).reshape(-1)   # alternate h, t per slot
 
 
