@@ -184,6 +184,8 @@ typedef struct kge_step_desc {
 
   void* workspace;
   uint64_t workspace_bytes;
+  void* const* prof_events;   /* optional: 4 hipEvent_t recorded before K0, KS,
+                                 KU and after KU (kernel timing; nullable)      */
 } kge_step_desc;
 
 /* ABI version compiled into the library. */

@@ -61,6 +61,7 @@ class kge_step_desc(ctypes.Structure):
         ("pos_score_out", ctypes.c_void_p), ("neg_score_out", ctypes.c_void_p),
         ("norm2_out", ctypes.c_void_p), ("status", ctypes.c_void_p),
         ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64),
+        ("prof_events", ctypes.c_void_p),
     ]
 
 

@@ -15,6 +15,7 @@ TF-2.5 IndexedSlices / clip_by_norm / optimizer semantics) runs:
     test-suite of the host logic).
 """
 
+import ctypes
 import os
 import warnings
 
@@ -140,20 +141,42 @@ class FusedStep:
             d.neg_score_out = neg_score.data_ptr()
         return d
 
-    def __call__(self, batch, is_train, optimizer, neg_ids=None, pos_score=None, neg_score=None):
+    def __call__(self, batch, is_train, optimizer, neg_ids=None, pos_score=None, neg_score=None,
+                 prof_events=None):
         if batch.device != self.device:
             batch = batch.to(self.device)
         if batch.dtype not in (torch.int32, torch.int64):
             batch = batch.to(torch.int64)
-        batch = batch.contiguous()
-        d = self.describe(batch, is_train, optimizer, neg_ids, pos_score, neg_score)
-        need = int(self.lib.kge_step_workspace_bytes(d))
-        if need == 0:   # invalid descriptor: kge_step re-validates and reports the status
-            _hip.check(self.lib.kge_step(d, _hip.stream_handle(self.device)), "kge_step")
-        if self.workspace.numel() < need:
-            self.workspace = torch.empty(need, dtype=torch.uint8, device=self.device)
-        d.workspace = self.workspace.data_ptr()
-        d.workspace_bytes = self.workspace.numel()
+        if not batch.is_contiguous():
+            batch = batch.contiguous()
+        m = self.model
+        key = (int(batch.shape[0]), batch.dtype, bool(is_train), id(optimizer),
+               getattr(optimizer, "learning_rate", None), neg_ids is not None,
+               pos_score is not None, neg_score is not None, m.model_weights["ent_emb"].data_ptr(),
+               id(m.ns_strategy), m.negative_ratio, m.corrupt_side)
+        cached = getattr(self, "_cache", None)
+        if cached is not None and cached[0] == key:
+            d = cached[1]
+            d.pos = batch.data_ptr()
+            if neg_ids is not None:
+                d.neg_ids = neg_ids.data_ptr()
+            else:
+                d.sampler.offset = m.ns_strategy.take_planes(2 if m.corrupt_side == "h+t" else 1)
+            if pos_score is not None:
+                d.pos_score_out = pos_score.data_ptr()
+            if neg_score is not None:
+                d.neg_score_out = neg_score.data_ptr()
+        else:
+            d = self.describe(batch, is_train, optimizer, neg_ids, pos_score, neg_score)
+            need = int(self.lib.kge_step_workspace_bytes(d))
+            if need == 0:   # invalid descriptor: kge_step re-validates and reports the status
+                _hip.check(self.lib.kge_step(d, _hip.stream_handle(self.device)), "kge_step")
+            if self.workspace.numel() < need:
+                self.workspace = torch.empty(need, dtype=torch.uint8, device=self.device)
+            d.workspace = self.workspace.data_ptr()
+            d.workspace_bytes = self.workspace.numel()
+            self._cache = (key, d)
+        d.prof_events = ctypes.cast(prof_events, ctypes.c_void_p) if prof_events is not None else None
         _hip.check(self.lib.kge_step(d, _hip.stream_handle(self.device)), "kge_step")
         return self.loss_out
 
@@ -168,12 +191,6 @@ class Tape:
 
     def __init__(self):
         self.records = []   # (name, flat idx, leaf)
-
-
-def _clip_scale(l2sum, clip):
-    # clip_ops.clip_by_norm: values * clip / max(norm, clip), norm = sqrt(l2sum) or 0
-    norm = torch.sqrt(l2sum) if float(l2sum) > 0 else torch.zeros_like(l2sum)
-    return clip / torch.maximum(norm, torch.as_tensor(clip, dtype=l2sum.dtype, device=l2sum.device))
 
 
 def _apply(name, w, opt, idx=None, values=None, dense=None):

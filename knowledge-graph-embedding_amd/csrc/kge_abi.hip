@@ -273,6 +273,8 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   A.sorted = (uint64_t*)(ws + P.o_sorted);
   A.starts = (int32_t*)(ws + P.o_starts);
 
+  hipEvent_t const* ev = (hipEvent_t const*)d->prof_events;
+  if (ev) (void)hipEventRecord(ev[0], st);
   // _constraint_loss assigns before scoring (BaseModel.py:319)
   const bool renorm = d->constraint && (d->model == KGE_MODEL_TRANSE || d->model == KGE_MODEL_DISTMULT);
   if (renorm) {
@@ -284,8 +286,10 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     (void)hipMemsetAsync(d->loss_out, 0, sizeof(float), st);
     return hip_check("kge_step(empty batch)");
   }
-  s = launch_step_elementwise(A, P.G, d->model, P.sk, st);
+  if (ev) (void)hipEventRecord(ev[1], st);
+  s = launch_step_elementwise(A, P.G, d->model, P.sk, st, ev);
   if (s != KGE_OK) return fail(s, "no kernel instance for model %d / score %d", d->model, P.sk);
+  if (ev) (void)hipEventRecord(ev[3], st);
   return hip_check("kge_step");
 }
 

@@ -55,7 +55,7 @@ struct StepGeom {
 };
 
 kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int model, int sk,
-                                   hipStream_t st);
+                                   hipStream_t st, hipEvent_t const* ev);
 
 __global__ void constrain_rows_kernel(float* t, int64_t rows, int32_t cols, int64_t ld, int kind,
                                       float value);

@@ -667,75 +667,76 @@ __global__ __launch_bounds__(256) void update_kernel(StepArgs A) {
 
 // ------------------------------------------------------------ dispatch
 template <template <int, int, int> class Model, int VEC, int NC, int SK>
-static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_t st) {
+static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_t st, hipEvent_t const* ev) {
   hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK>), dim3(G.nWG), dim3(256), G.lds_score, st, A);
+  if (ev) (void)hipEventRecord(ev[2], st);
   hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK>), dim3(A.train ? G.gridU : 1), dim3(256),
                      G.lds_update, st, A);
   return KGE_OK;
 }
 
 template <template <int, int, int> class Model, int VEC, int NC>
-static kge_status by_sk(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st) {
+static kge_status by_sk(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st, hipEvent_t const* ev) {
   switch (sk) {
-    case SK_P1: return launch_family<Model, VEC, NC, SK_P1>(A, G, st);
-    case SK_P2: return launch_family<Model, VEC, NC, SK_P2>(A, G, st);
-    case SK_PINF: return launch_family<Model, VEC, NC, SK_PINF>(A, G, st);
-    default: return launch_family<Model, VEC, NC, SK_DOT>(A, G, st);
+    case SK_P1: return launch_family<Model, VEC, NC, SK_P1>(A, G, st, ev);
+    case SK_P2: return launch_family<Model, VEC, NC, SK_P2>(A, G, st, ev);
+    case SK_PINF: return launch_family<Model, VEC, NC, SK_PINF>(A, G, st, ev);
+    default: return launch_family<Model, VEC, NC, SK_DOT>(A, G, st, ev);
   }
 }
 
 template <template <int, int, int> class Model, int VEC, int NC>
-static kge_status by_sk_lp(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st) {
+static kge_status by_sk_lp(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st, hipEvent_t const* ev) {
   switch (sk) {
-    case SK_P1: return launch_family<Model, VEC, NC, SK_P1>(A, G, st);
-    case SK_P2: return launch_family<Model, VEC, NC, SK_P2>(A, G, st);
-    case SK_PINF: return launch_family<Model, VEC, NC, SK_PINF>(A, G, st);
+    case SK_P1: return launch_family<Model, VEC, NC, SK_P1>(A, G, st, ev);
+    case SK_P2: return launch_family<Model, VEC, NC, SK_P2>(A, G, st, ev);
+    case SK_PINF: return launch_family<Model, VEC, NC, SK_PINF>(A, G, st, ev);
     default: return KGE_EUNSUPPORTED;
   }
 }
 
 // TransE: every score kind, VEC 4 / 1
-static kge_status transe(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st) {
+static kge_status transe(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st, hipEvent_t const* ev) {
   if (G.vec == 4) {
-    if (G.nc == 1) return by_sk<TransE, 4, 1>(A, G, sk, st);
-    if (G.nc == 2) return by_sk<TransE, 4, 2>(A, G, sk, st);
-    return by_sk<TransE, 4, 4>(A, G, sk, st);
+    if (G.nc == 1) return by_sk<TransE, 4, 1>(A, G, sk, st, ev);
+    if (G.nc == 2) return by_sk<TransE, 4, 2>(A, G, sk, st, ev);
+    return by_sk<TransE, 4, 4>(A, G, sk, st, ev);
   }
-  if (G.nc == 1) return by_sk<TransE, 1, 1>(A, G, sk, st);
-  if (G.nc == 2) return by_sk<TransE, 1, 2>(A, G, sk, st);
-  return by_sk<TransE, 1, 4>(A, G, sk, st);
+  if (G.nc == 1) return by_sk<TransE, 1, 1>(A, G, sk, st, ev);
+  if (G.nc == 2) return by_sk<TransE, 1, 2>(A, G, sk, st, ev);
+  return by_sk<TransE, 1, 4>(A, G, sk, st, ev);
 }
 
 // DistMult: its own trilinear score (score_fn unused), VEC 4 / 1
-static kge_status distmult(const StepArgs& A, const StepGeom& G, hipStream_t st) {
+static kge_status distmult(const StepArgs& A, const StepGeom& G, hipStream_t st, hipEvent_t const* ev) {
   if (G.vec == 4) {
-    if (G.nc == 1) return launch_family<DistMult, 4, 1, SK_DOT>(A, G, st);
-    if (G.nc == 2) return launch_family<DistMult, 4, 2, SK_DOT>(A, G, st);
-    return launch_family<DistMult, 4, 4, SK_DOT>(A, G, st);
+    if (G.nc == 1) return launch_family<DistMult, 4, 1, SK_DOT>(A, G, st, ev);
+    if (G.nc == 2) return launch_family<DistMult, 4, 2, SK_DOT>(A, G, st, ev);
+    return launch_family<DistMult, 4, 4, SK_DOT>(A, G, st, ev);
   }
-  if (G.nc == 1) return launch_family<DistMult, 1, 1, SK_DOT>(A, G, st);
-  if (G.nc == 2) return launch_family<DistMult, 1, 2, SK_DOT>(A, G, st);
-  return launch_family<DistMult, 1, 4, SK_DOT>(A, G, st);
+  if (G.nc == 1) return launch_family<DistMult, 1, 1, SK_DOT>(A, G, st, ev);
+  if (G.nc == 2) return launch_family<DistMult, 1, 2, SK_DOT>(A, G, st, ev);
+  return launch_family<DistMult, 1, 4, SK_DOT>(A, G, st, ev);
 }
 
 // RotatE: Lp kinds on complex rows, VEC 4 / 2 (a complex pair never splits)
-static kge_status rotate(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st) {
+static kge_status rotate(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st, hipEvent_t const* ev) {
   if (G.vec == 4) {
-    if (G.nc == 1) return by_sk_lp<RotatE, 4, 1>(A, G, sk, st);
-    if (G.nc == 2) return by_sk_lp<RotatE, 4, 2>(A, G, sk, st);
-    return by_sk_lp<RotatE, 4, 4>(A, G, sk, st);
+    if (G.nc == 1) return by_sk_lp<RotatE, 4, 1>(A, G, sk, st, ev);
+    if (G.nc == 2) return by_sk_lp<RotatE, 4, 2>(A, G, sk, st, ev);
+    return by_sk_lp<RotatE, 4, 4>(A, G, sk, st, ev);
   }
-  if (G.nc == 1) return by_sk_lp<RotatE, 2, 1>(A, G, sk, st);
-  if (G.nc == 2) return by_sk_lp<RotatE, 2, 2>(A, G, sk, st);
-  return by_sk_lp<RotatE, 2, 4>(A, G, sk, st);
+  if (G.nc == 1) return by_sk_lp<RotatE, 2, 1>(A, G, sk, st, ev);
+  if (G.nc == 2) return by_sk_lp<RotatE, 2, 2>(A, G, sk, st, ev);
+  return by_sk_lp<RotatE, 2, 4>(A, G, sk, st, ev);
 }
 
 kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int model, int sk,
-                                   hipStream_t st) {
+                                   hipStream_t st, hipEvent_t const* ev) {
   switch (model) {
-    case KGE_MODEL_TRANSE: return transe(A, G, sk, st);
-    case KGE_MODEL_DISTMULT: return distmult(A, G, st);
-    case KGE_MODEL_ROTATE: return rotate(A, G, sk, st);
+    case KGE_MODEL_TRANSE: return transe(A, G, sk, st, ev);
+    case KGE_MODEL_DISTMULT: return distmult(A, G, st, ev);
+    case KGE_MODEL_ROTATE: return rotate(A, G, sk, st, ev);
     default: return KGE_EUNSUPPORTED;
   }
 }

@@ -296,10 +296,10 @@ def _constraint(model, W, L, X, cfg, batch_scale):
 
 def train_step(model, weights, pos, neg_ids, score=("lp", 2.0), loss=("hinge", 1.0), lr=0.01, constraint=True,
                constraint_weight=1.0, side="h+t", train=True, batch_scale=1.0, limit=None,
-               clip_norm=5.0):
+               clip_norm=5.0, dtype=F64):
     """One reference step with injected negatives. Returns dict with loss,
     pos_score, neg_score, weights (numpy, updated) and norm2 per variable."""
-    W = {k: torch.tensor(np.asarray(v), dtype=F64) for k, v in weights.items()}
+    W = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in weights.items()}
     names = list(W.keys())
     pos = np.asarray(pos, dtype=np.int64)
     B = len(pos)
@@ -315,7 +315,7 @@ def train_step(model, weights, pos, neg_ids, score=("lp", 2.0), loss=("hinge", 1
         ps = _score_hrt(model, W, L, pos[:, 0], pos[:, 1], pos[:, 2], score, cfg)
         ns = _score_hrt(model, W, L, negt[:, 0], negt[:, 1], negt[:, 2], score, cfg)
         lval = loss_fn(loss, ps, ns, batch_scale) + cterm
-    out = {"loss": float(lval), "pos_score": ps.detach().numpy(), "neg_score": ns.detach().numpy(),
+    out = {"loss": float(lval.detach()), "pos_score": ps.detach().numpy(), "neg_score": ns.detach().numpy(),
            "norm2": {}}
     if train:
         leaves = [x[2] for x in L.rec]
