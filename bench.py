@@ -10,8 +10,10 @@ clip -> sparse SGD update) on a batch already resident in HBM.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 one process per GPU, each with its own 1024-positive batch (weak scaling, the
-global batch is N*1024), entity/relation tables replicated, gradients summed
-with RCCL all-reduce before the (identical) update on every rank.
+global batch is N*1024); the entity table is row-sharded across the ranks
+(KGE/sharded.py: all-gather of the shards, fused gradient step, RCCL
+reduce-scatter of the entity gradient + all-reduce of the relation gradient,
+global clip norm and loss, sharded SGD apply).
 
 Prints ONE JSON line (rank 0).
 """
@@ -129,7 +131,8 @@ def main():
     model._to_device()
     opt = optimizers.SGD(learning_rate=0.01)
     if world > 1:
-        step = engine.DistributedFusedStep(model)
+        from KGE.sharded import ShardedStep
+        step = ShardedStep(model)
     else:
         step = engine.FusedStep(model)
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define KGE_ABI_VERSION 1
+#define KGE_ABI_VERSION 2
 
 typedef enum kge_status {
   KGE_OK = 0,
@@ -84,8 +84,22 @@ enum {
   KGE_SAMPLER_GIVEN = 2    /* negatives supplied by the caller (neg_ids input) */
 };
 
-/* optimizer applied by the step (BaseModel.py:325-328) */
-enum { KGE_OPT_NONE = 0, KGE_OPT_SGD = 1 };
+/* optimizer applied by the step (BaseModel.py:325-328)
+ *  KGE_OPT_NONE  validation step (BaseModel.py:141-145): loss only
+ *  KGE_OPT_SGD   keras SGD sparse apply (ResourceScatterAdd(var, idx, -lr*clip(g)))
+ *  KGE_OPT_GRAD  no update: the step writes each variable's duplicate-summed,
+ *                UN-clipped gradient into the dense buffers grad_out[v] (rows not
+ *                touched are zeroed) and its slice norm^2 into norm2_out[v];
+ *                kge_apply() then clips and applies it (Adam, or a multi-GPU
+ *                step that reduces gradients across ranks first).
+ *  KGE_OPT_ADAM  kge_apply() only: keras Adam (OptimizerV2, TF 2.5). */
+enum { KGE_OPT_NONE = 0, KGE_OPT_SGD = 1, KGE_OPT_GRAD = 2, KGE_OPT_ADAM = 3 };
+
+/* kge_step_desc.flags */
+enum {
+  KGE_FLAG_NO_TABLE_CONSTRAINT = 1  /* caller already applied the full-table
+                                       _constraint_loss assigns (e.g. on its shard) */
+};
 
 typedef struct kge_table {
   float* data;   /* device pointer, row-major                    */
@@ -186,7 +200,37 @@ typedef struct kge_step_desc {
   uint64_t workspace_bytes;
   void* const* prof_events;   /* optional: 4 hipEvent_t recorded before K0, KS,
                                  KU and after KU (kernel timing; nullable)      */
+  int32_t flags;              /* KGE_FLAG_*                                     */
+  int32_t _pad;
+  float* grad_out[4];         /* KGE_OPT_GRAD: dense [rows, cols] gradient per
+                                 variable (order as norm2_out; row stride cols) */
 } kge_step_desc;
+
+/*
+ * Optimizer apply for one variable (BaseModel.py:327-328): clip_by_norm(g,
+ * clip_norm) with the variable's global slice norm (TF-2.5 IndexedSlices:
+ * duplicates not summed), then
+ *   SGD : var -= lr * clip(g)                         (rows with g == 0 unchanged)
+ *   ADAM: m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g^2  over ALL rows (keras
+ *         sparse Adam decays every row), var -= lr_t * m / (sqrt(v) + eps),
+ *         lr_t = lr * sqrt(1 - b2^t) / (1 - b1^t).
+ * g is the duplicate-summed gradient written by a KGE_OPT_GRAD step (and
+ * reduced across ranks by the caller, if any).
+ */
+typedef struct kge_apply_desc {
+  int32_t optimizer;          /* KGE_OPT_SGD or KGE_OPT_ADAM                    */
+  int32_t _pad;
+  kge_table var;              /* rows to update (a whole table or one shard)   */
+  const float* grad;          /* [var.rows, var.cols], row stride var.cols     */
+  const float* norm2;         /* device [1]: ||g slices||^2 of this variable   */
+  float lr;
+  float clip_norm;
+  float* m;                   /* ADAM slots [var.rows, var.cols], stride cols  */
+  float* v;
+  float beta_1, beta_2, epsilon;
+  int32_t _pad2;
+  int64_t iteration;          /* ADAM step t >= 1 (optimizer.iterations + 1)   */
+} kge_apply_desc;
 
 /* ABI version compiled into the library. */
 int32_t kge_abi_version(void);
@@ -202,6 +246,9 @@ kge_status kge_step(const kge_step_desc* d, void* stream);
 
 /* Standalone negative sampling (ns_strategy.py:39-64, :94-132). */
 kge_status kge_sample(const kge_sample_desc* d, void* stream);
+
+/* Optimizer apply of one variable (see kge_apply_desc). */
+kge_status kge_apply(const kge_apply_desc* d, void* stream);
 
 /* Row constraints over a whole table (constraint.py:4-31, :70-99):
  * kind 0 = normalized_embeddings(p=2, value), 1 = clip_constraint(p=2, value).

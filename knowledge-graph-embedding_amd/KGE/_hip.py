@@ -11,7 +11,7 @@ import threading
 
 import torch
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 KGE_OK, KGE_EINVAL, KGE_ERANGE, KGE_EHIP, KGE_ENOMEM_WORKSPACE, KGE_EUNSUPPORTED = range(6)
 
@@ -19,7 +19,8 @@ MODEL_TRANSE, MODEL_TRANSH, MODEL_TRANSR, MODEL_TRANSD, MODEL_ROTATE, MODEL_DIST
 SIDE_H, SIDE_T, SIDE_HT = range(3)
 IDX_I32, IDX_I64 = range(2)
 SAMPLER_UNIFORM, SAMPLER_TYPED, SAMPLER_GIVEN = range(3)
-OPT_NONE, OPT_SGD = range(2)
+OPT_NONE, OPT_SGD, OPT_GRAD, OPT_ADAM = range(4)
+FLAG_NO_TABLE_CONSTRAINT = 1
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libkge_hip.so")
 
@@ -62,11 +63,21 @@ class kge_step_desc(ctypes.Structure):
         ("norm2_out", ctypes.c_void_p), ("status", ctypes.c_void_p),
         ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_uint64),
         ("prof_events", ctypes.c_void_p),
+        ("flags", ctypes.c_int32), ("_pad", ctypes.c_int32),
+        ("grad_out", ctypes.c_void_p * 4),
     ]
 
 
+class kge_apply_desc(ctypes.Structure):
+    _fields_ = [("optimizer", ctypes.c_int32), ("_pad", ctypes.c_int32), ("var", kge_table),
+                ("grad", ctypes.c_void_p), ("norm2", ctypes.c_void_p), ("lr", ctypes.c_float),
+                ("clip_norm", ctypes.c_float), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p),
+                ("beta_1", ctypes.c_float), ("beta_2", ctypes.c_float), ("epsilon", ctypes.c_float),
+                ("_pad2", ctypes.c_int32), ("iteration", ctypes.c_int64)]
+
+
 EXPORTS = ("kge_abi_version", "kge_last_error", "kge_step_workspace_bytes", "kge_step", "kge_sample",
-           "kge_constrain_rows")
+           "kge_apply", "kge_constrain_rows")
 
 _lock = threading.Lock()
 _lib = None
@@ -91,6 +102,8 @@ def load(path=LIB_PATH):
         L.kge_step.argtypes = [ctypes.POINTER(kge_step_desc), ctypes.c_void_p]
         L.kge_sample.restype = ctypes.c_int
         L.kge_sample.argtypes = [ctypes.POINTER(kge_sample_desc), ctypes.c_void_p]
+        L.kge_apply.restype = ctypes.c_int
+        L.kge_apply.argtypes = [ctypes.POINTER(kge_apply_desc), ctypes.c_void_p]
         L.kge_constrain_rows.restype = ctypes.c_int
         L.kge_constrain_rows.argtypes = [kge_table, ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]
         if L.kge_abi_version() != ABI_VERSION:

@@ -49,7 +49,7 @@ def fused_plan(model, optimizer):
         return "KGE_BACKEND=eager"
     if getattr(model, "_fused_model_id", None) is None:
         return "%s has no fused kernel" % type(model).__name__
-    if model._fused_model_id not in (_hip.MODEL_TRANSE, _hip.MODEL_DISTMULT, _hip.MODEL_ROTATE):
+    if model._fused_model_id not in FUSED_MODELS:
         return "%s has no fused kernel in this build" % type(model).__name__
     if hasattr(model, "score_fn"):
         sd = _score.fused_descriptor(model.score_fn)
@@ -61,32 +61,89 @@ def fused_plan(model, optimizer):
         return "custom loss function"
     if type(model.ns_strategy) not in (_ns.UniformStrategy, _ns.TypedStrategy):
         return "custom negative sampler"
-    if optimizer is not None and not isinstance(optimizer, _opt.SGD):
-        return "%s optimizer is not fused yet" % type(optimizer).__name__
+    if optimizer is not None and not isinstance(optimizer, (_opt.SGD, _opt.Adam)):
+        return "%s optimizer has no fused apply" % type(optimizer).__name__
     return None
 
 
-class FusedStep:
-    """Device buffers + descriptor for one model's ``kge_step`` calls."""
+FUSED_MODELS = (_hip.MODEL_TRANSE, _hip.MODEL_DISTMULT, _hip.MODEL_ROTATE)
 
-    def __init__(self, model):
+
+def fused_names(model):
+    """model_weights keys of the fused step's tables, by role."""
+    t = model._fused_tables()
+    out = {}
+    for role in ("ent", "rel", "ent_aux", "rel_aux"):
+        x = t.get(role)
+        if x is None:
+            continue
+        out[role] = next(k for k, w in model.model_weights.items() if w is x)
+    return out
+
+
+def _rows_cols(t):
+    return int(t.shape[0]), int(t.numel() // max(int(t.shape[0]), 1))
+
+
+class FusedStep:
+    """Device buffers + descriptor for one model's ``kge_step`` calls.
+
+    SGD runs entirely inside ``kge_step`` (sparse update in its second
+    kernel). Adam runs ``kge_step`` in ``KGE_OPT_GRAD`` mode (dense
+    duplicate-summed gradients + per-variable slice norm^2) followed by one
+    ``kge_apply`` per variable (keras sparse Adam decays every row).
+    ``grad_mode=True`` always stops after the gradients (multi-GPU exchange).
+    """
+
+    def __init__(self, model, grad_mode=False, tables=None):
         self.model = model
-        dev = model.model_weights["ent_emb"].device
+        self.tables = tables          # optional override of model._fused_tables()
+        t = self._tables()
+        dev = t["ent"].device
         if dev.type != "cuda":
             raise RuntimeError("the fused step needs the model on a GPU (got %s); set KGE_BACKEND=eager "
                                "for host-only runs" % dev)
         self.device = dev
         self.lib = _hip.lib()      # raises if libkge_hip.so is missing
+        self.grad_mode = grad_mode
         self.loss_out = torch.zeros(1, dtype=torch.float32, device=dev)
         self.loss_accum = torch.zeros(1, dtype=torch.float32, device=dev)
         self.norm2 = torch.zeros(4, dtype=torch.float32, device=dev)
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.workspace = torch.empty(0, dtype=torch.uint8, device=dev)
+        self.grads = None
         self.batch_scale = 1.0
+        self.flags = 0
+        self.plane_fn = None          # optional: planes -> first plane (multi-GPU offsets)
+
+    def _tables(self):
+        return self.tables if self.tables is not None else self.model._fused_tables()
+
+    def grad_buffers(self):
+        """Dense [rows, cols] gradient buffers of the ent / rel tables (KGE_OPT_GRAD)."""
+        if self.grads is None:
+            t = self._tables()
+            self.grads = [torch.zeros(_rows_cols(t[k]), dtype=torch.float32, device=self.device)
+                          for k in ("ent", "rel")]
+        return self.grads
+
+    def _opt_code(self, is_train, optimizer):
+        if not is_train:
+            return _hip.OPT_NONE
+        if self.grad_mode or isinstance(optimizer, _opt.Adam):
+            return _hip.OPT_GRAD
+        return _hip.OPT_SGD
+
+    def _planes(self):
+        m = self.model
+        n = 2 if m.corrupt_side == "h+t" else 1
+        if self.plane_fn is not None:
+            return self.plane_fn(m.ns_strategy, n)
+        return m.ns_strategy.take_planes(n)
 
     def describe(self, batch, is_train, optimizer, neg_ids=None, pos_score=None, neg_score=None):
         m = self.model
-        t = m._fused_tables()
+        t = self._tables()
         d = _hip.kge_step_desc()
         d.abi_version = _hip.ABI_VERSION
         d.model = m._fused_model_id
@@ -108,9 +165,7 @@ class FusedStep:
             d.sampler.idx_dtype = d.idx_dtype
             d.neg_ids = neg_ids.data_ptr()
         else:
-            planes = 2 if m.corrupt_side == "h+t" else 1
-            plane = m.ns_strategy.take_planes(planes)
-            d.sampler = m.ns_strategy.sampler_desc(d.idx_dtype, self.device, plane)
+            d.sampler = m.ns_strategy.sampler_desc(d.idx_dtype, self.device, self._planes())
         if hasattr(m, "score_fn"):
             kind, p = _score.fused_descriptor(m.score_fn)
         else:
@@ -125,12 +180,15 @@ class FusedStep:
         d.constraint = int(bool(getattr(m, "constraint", False)))
         d.constraint_weight = float(getattr(m, "constraint_weight", 0.0))
         d.rotate_limit = float(t.get("limit", 0.0))
-        if is_train:
-            d.optimizer = _hip.OPT_SGD
+        d.optimizer = self._opt_code(is_train, optimizer)
+        if d.optimizer == _hip.OPT_SGD:
             d.lr = optimizer.learning_rate
-        else:
-            d.optimizer = _hip.OPT_NONE
         d.clip_norm = 5.0
+        d.flags = self.flags
+        if d.optimizer == _hip.OPT_GRAD:
+            g = self.grad_buffers()
+            d.grad_out[0] = g[0].data_ptr()
+            d.grad_out[1] = g[1].data_ptr()
         d.loss_out = self.loss_out.data_ptr()
         d.loss_accum = self.loss_accum.data_ptr()
         d.norm2_out = self.norm2.data_ptr()
@@ -150,10 +208,11 @@ class FusedStep:
         if not batch.is_contiguous():
             batch = batch.contiguous()
         m = self.model
+        t = self._tables()
         key = (int(batch.shape[0]), batch.dtype, bool(is_train), id(optimizer),
                getattr(optimizer, "learning_rate", None), neg_ids is not None,
-               pos_score is not None, neg_score is not None, m.model_weights["ent_emb"].data_ptr(),
-               id(m.ns_strategy), m.negative_ratio, m.corrupt_side)
+               pos_score is not None, neg_score is not None, t["ent"].data_ptr(), t["rel"].data_ptr(),
+               id(m.ns_strategy), m.negative_ratio, m.corrupt_side, self.batch_scale, self.flags)
         cached = getattr(self, "_cache", None)
         if cached is not None and cached[0] == key:
             d = cached[1]
@@ -161,7 +220,7 @@ class FusedStep:
             if neg_ids is not None:
                 d.neg_ids = neg_ids.data_ptr()
             else:
-                d.sampler.offset = m.ns_strategy.take_planes(2 if m.corrupt_side == "h+t" else 1)
+                d.sampler.offset = self._planes()
             if pos_score is not None:
                 d.pos_score_out = pos_score.data_ptr()
             if neg_score is not None:
@@ -178,7 +237,36 @@ class FusedStep:
             self._cache = (key, d)
         d.prof_events = ctypes.cast(prof_events, ctypes.c_void_p) if prof_events is not None else None
         _hip.check(self.lib.kge_step(d, _hip.stream_handle(self.device)), "kge_step")
+        if is_train and isinstance(optimizer, _opt.Adam) and not self.grad_mode:
+            self.apply_adam(optimizer)
         return self.loss_out
+
+    def apply(self, var, grad, norm2_ptr, optimizer, name=None):
+        """``kge_apply`` of one variable (SGD or keras Adam) with global norm^2 at ``norm2_ptr``."""
+        a = _hip.kge_apply_desc()
+        a.var = _hip.table(var)
+        a.grad = grad.data_ptr()
+        a.norm2 = norm2_ptr
+        a.lr = optimizer.learning_rate
+        a.clip_norm = 5.0
+        if isinstance(optimizer, _opt.Adam):
+            st = optimizer.slots.setdefault(name, {"m": torch.zeros_like(var), "v": torch.zeros_like(var)})
+            a.optimizer = _hip.OPT_ADAM
+            a.m = st["m"].data_ptr()
+            a.v = st["v"].data_ptr()
+            a.beta_1, a.beta_2, a.epsilon = optimizer.beta_1, optimizer.beta_2, optimizer.epsilon
+            a.iteration = optimizer.iterations
+        else:
+            a.optimizer = _hip.OPT_SGD
+        _hip.check(self.lib.kge_apply(a, _hip.stream_handle(self.device)), "kge_apply")
+
+    def apply_adam(self, optimizer):
+        optimizer.iterations += 1
+        t = self._tables()
+        names = fused_names(self.model)
+        g = self.grad_buffers()
+        for v, role in enumerate(("ent", "rel")):
+            self.apply(t[role], g[v], self.norm2.data_ptr() + 4 * v, optimizer, names[role])
 
     def check_status(self):
         _hip.check_device_status(self.status, "kge_step")
@@ -220,8 +308,10 @@ def _apply(name, w, opt, idx=None, values=None, dense=None):
         w.sub_(lr_t * m / (torch.sqrt(v) + opt.epsilon))
 
 
-def eager_step(model, batch, is_train, optimizer, neg=None, batch_scale=1.0):
-    """Reference step order (BaseModel.py:316-328) with TF-2.5 gradient semantics."""
+def eager_grads(model, batch, is_train, neg=None, batch_scale=1.0):
+    """Steps 1-5 of the reference step (BaseModel.py:316-326) with TF-2.5
+    gradient semantics. Returns (loss, {name: ("dense", g) | ("slices", idx, values)});
+    the gradient dict is empty for a validation step."""
     weights = model.model_weights
     if neg is None:
         neg = model._negative_sampling(batch)
@@ -238,7 +328,7 @@ def eager_step(model, batch, is_train, optimizer, neg=None, batch_scale=1.0):
             neg_score = model.score_hrt(neg[:, 0], neg[:, 1], neg[:, 2])
             batch_loss = _call_loss(model.loss_fn, pos_score, neg_score, batch_scale) + constraint_term
         if not is_train:
-            return batch_loss.detach().reshape(())
+            return batch_loss.detach().reshape(()), {}
         names = list(weights.keys())
         params = [weights[n] for n in names]
         leaves = [r[2] for r in tape.records]
@@ -253,10 +343,8 @@ def eager_step(model, batch, is_train, optimizer, neg=None, batch_scale=1.0):
         model._tape = None
         for w in weights.values():
             w.requires_grad_(False)
-    if isinstance(optimizer, _opt.Adam):
-        optimizer.iterations += 1
+    out = {}
     for name in names:
-        w = weights[name]
         sl = slices.get(name, [])
         dg = dense.get(name)
         if dg is None and not sl:
@@ -265,18 +353,44 @@ def eager_step(model, batch, is_train, optimizer, neg=None, batch_scale=1.0):
             total = dg.clone()
             for idx, g in sl:
                 total.index_add_(0, idx, g)
-            total = total * 5.0 / torch.maximum(_norm_or_zero(total), torch.tensor(5.0, device=total.device))
-            _apply(name, w, optimizer, dense=total)
+            out[name] = ("dense", total)
         else:
-            idx = torch.cat([i for i, _ in sl])
-            vals = torch.cat([g for _, g in sl])
-            vals = vals * 5.0 / torch.maximum(_norm_or_zero(vals), torch.tensor(5.0, device=vals.device))
-            _apply(name, w, optimizer, idx=idx, values=vals)
-    return batch_loss.detach().reshape(())
+            out[name] = ("slices", torch.cat([i for i, _ in sl]), torch.cat([g for _, g in sl]))
+    return batch_loss.detach().reshape(()), out
 
 
-def _norm_or_zero(x):
-    l2 = torch.sum(x * x)
+def grad_norm2(g):
+    """Squared L2 norm clip_by_norm sees: over the slice values (not de-duplicated)."""
+    x = g[1] if g[0] == "dense" else g[2]
+    return torch.sum(x * x)
+
+
+def dense_grad(g, like):
+    """Duplicate-summed dense gradient of a variable shaped like ``like``."""
+    if g[0] == "dense":
+        return g[1]
+    return torch.zeros_like(like).index_add_(0, g[1], g[2])
+
+
+def eager_step(model, batch, is_train, optimizer, neg=None, batch_scale=1.0):
+    """Reference step order (BaseModel.py:316-328) with TF-2.5 gradient semantics."""
+    loss, grads = eager_grads(model, batch, is_train, neg, batch_scale)
+    if not is_train:
+        return loss
+    if isinstance(optimizer, _opt.Adam):
+        optimizer.iterations += 1
+    for name, g in grads.items():
+        w = model.model_weights[name]
+        n2 = grad_norm2(g)
+        scale = 5.0 / torch.maximum(_sqrt_or_zero(n2), torch.tensor(5.0, device=w.device))
+        if g[0] == "dense":
+            _apply(name, w, optimizer, dense=g[1] * scale)
+        else:
+            _apply(name, w, optimizer, idx=g[1], values=g[2] * scale)
+    return loss
+
+
+def _sqrt_or_zero(l2):
     return torch.where(l2 > 0, torch.sqrt(torch.where(l2 > 0, l2, torch.ones_like(l2))), l2)
 
 

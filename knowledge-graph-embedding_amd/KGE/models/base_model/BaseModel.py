@@ -35,6 +35,11 @@ from ...ns_strategy import TypedStrategy, UniformStrategy
 logging.getLogger().setLevel(logging.INFO)
 
 
+def _world_size():
+    d = torch.distributed
+    return d.get_world_size() if d.is_available() and d.is_initialized() else 1
+
+
 class KGEModel:
     """Base class for KGE models (``BaseModel.py:23-56``)."""
 
@@ -103,6 +108,7 @@ class KGEModel:
                     break
             else:
                 self._save_checkpoint()
+        self.sync_weights()
         self.train_loss_history = train_loss_history
         self.val_loss_history = val_loss_history
         if log_projector:
@@ -156,13 +162,31 @@ class KGEModel:
         """One batch (``BaseModel.py:293-330``); returns the loss as a device scalar."""
         opt = self._optimizer if is_train else None
         reason = engine.fused_plan(self, opt)
+        world = _world_size()
         if reason is None:
             if self._fused is None:
-                self._fused = engine.FusedStep(self)
+                if world > 1:
+                    from ...sharded import ShardedStep
+                    self._fused = ShardedStep(self)
+                else:
+                    self._fused = engine.FusedStep(self)
+            if world > 1:
+                # every rank draws the same global batch; each scores its slice
+                n = batch_data.shape[0]
+                assert n % world == 0, "batch_size must be divisible by the world size"
+                rank = torch.distributed.get_rank()
+                batch_data = batch_data[rank * (n // world):(rank + 1) * (n // world)]
             return self._fused(batch_data, is_train, opt).clone().reshape(()).to(torch.float64)
+        if world > 1:
+            raise NotImplementedError("multi-GPU training needs a fused combination (%s)" % reason)
         if engine.backend() != "eager":
             engine.warn_once((type(self).__name__, reason), "eager plugin path: %s" % reason)
         return engine.eager_step(self, batch_data, is_train, opt).to(torch.float64)
+
+    def sync_weights(self):
+        """Multi-GPU: gather the entity shards into ``model_weights`` (before evaluation)."""
+        if self._fused is not None and hasattr(self._fused, "sync"):
+            self._fused.sync()
 
     def _check_device_status(self):
         if self._fused is not None:

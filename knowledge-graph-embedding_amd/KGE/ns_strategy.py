@@ -8,8 +8,9 @@ reference never seeds TF's RNG, so its draws are not).
 
 CUDA tensors are sampled by ``kge_sample`` in ``libkge_hip.so``; the fused
 training step draws the same ids in-kernel from the same planes. CPU tensors
-are sampled on the host with the identical spec (``_philox.py``) for the
-eager plugin path.
+are refused (RuntimeError) unless the host-development backend is selected
+explicitly (``KGE_BACKEND=eager``), which samples on the host with the
+identical spec (``_philox.py``): there is no silent CPU fallback.
 """
 
 import os
@@ -92,6 +93,7 @@ class UniformStrategy(_CounterSampler):
         plane = self.take_planes(1)
         if X.is_cuda:
             return _sample_cuda(self.sampler_desc(_idx_code(X), X.device, plane), X, negative_ratio, side)
+        _host_allowed("UniformStrategy")
         idx = _philox.draw(self.seed, plane, np.arange(n * negative_ratio), X.dtype == torch.int64, self.n)
         out = self.sample_pool.numpy()[idx] if not self.identity else idx
         return torch.from_numpy(np.asarray(out)).to(X.dtype)
@@ -188,9 +190,16 @@ class TypedStrategy(_CounterSampler):
         plane = self.take_planes(1)
         if X.is_cuda:
             return _sample_cuda(self.sampler_desc(_idx_code(X), X.device, plane), X, negative_ratio, side)
+        _host_allowed("TypedStrategy")
         col = 0 if side == "h" else 2
         out = self.draw_host(X[:, col].numpy(), plane, negative_ratio, X.dtype == torch.int64)
         return torch.from_numpy(np.asarray(out)).to(X.dtype)
+
+
+def _host_allowed(what):
+    if os.environ.get("KGE_BACKEND", "fused").lower() != "eager":
+        raise RuntimeError("%s: CPU tensors are sampled only with KGE_BACKEND=eager (host development); "
+                           "move the triples to the GPU to use kge_sample" % what)
 
 
 def _idx_code(X):

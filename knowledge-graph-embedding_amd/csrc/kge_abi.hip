@@ -94,9 +94,12 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     return fail(KGE_EUNSUPPORTED, "RotatE with Dot() yields a complex score");
   if (model == KGE_MODEL_ROTATE && !(d->rotate_limit > 0.f))
     return fail(KGE_EINVAL, "RotatE rotate_limit must be > 0");
-  if (d->optimizer != KGE_OPT_NONE && d->optimizer != KGE_OPT_SGD)
-    return fail(KGE_EUNSUPPORTED, "optimizer %d has no fused kernel in this build", d->optimizer);
+  if (d->optimizer != KGE_OPT_NONE && d->optimizer != KGE_OPT_SGD && d->optimizer != KGE_OPT_GRAD)
+    return fail(KGE_EINVAL, "kge_step optimizer must be NONE, SGD or GRAD (got %d)", d->optimizer);
   if (d->optimizer == KGE_OPT_SGD && !(d->clip_norm > 0.f)) return fail(KGE_EINVAL, "clip_norm must be > 0");
+  if (d->optimizer == KGE_OPT_GRAD && (!d->grad_out[0] || !d->grad_out[1]))
+    return fail(KGE_EINVAL, "KGE_OPT_GRAD needs grad_out[0] (ent) and grad_out[1] (rel)");
+  if (d->optimizer == KGE_OPT_GRAD && !d->norm2_out) return fail(KGE_EINVAL, "KGE_OPT_GRAD needs norm2_out");
   if (!d->loss_out) return fail(KGE_EINVAL, "null loss_out");
   const kge_sampler_desc& sm = d->sampler;
   if (sm.kind == KGE_SAMPLER_GIVEN) {
@@ -169,6 +172,9 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.pos = d->pos;
   A.i64 = d->idx_dtype == KGE_IDX_I64;
   A.train = d->optimizer != KGE_OPT_NONE;
+  A.grad_mode = d->optimizer == KGE_OPT_GRAD;
+  A.gent = d->grad_out[0];
+  A.grel = d->grad_out[1];
   A.given = sm.kind == KGE_SAMPLER_GIVEN;
   A.pw = d->score_kind == KGE_SCORE_LP_POW;
   A.rel_half = model == KGE_MODEL_ROTATE;
@@ -241,9 +247,62 @@ __global__ __launch_bounds__(256) void sample_kernel(SamplerView s, const void* 
   if (err) set_status(status, err);
 }
 
+// ------------------------------------------------------------ apply kernels
+// var += -lr * clip * g  (SGD) ; keras Adam over every element (ADAM).
+__global__ __launch_bounds__(256) void apply_kernel(float* __restrict__ w, int64_t rows, int32_t cols, int64_t ld,
+                                                     const float* __restrict__ g, const float* __restrict__ norm2,
+                                                     float lr, float clip, int adam, float* __restrict__ m,
+                                                     float* __restrict__ v, float b1, float b2, float eps,
+                                                     float lr_t) {
+  const float n = sqrtf(*norm2);
+  const float cs = clip / fmaxf(n, clip);
+  const int64_t total = rows * (int64_t)cols;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = q / cols;
+    const int c = (int)(q - r * cols);
+    const float gv = g[q] * cs;
+    float* wp = w + r * ld + c;
+    if (!adam) {
+      *wp = *wp + gv * (-lr);
+    } else {
+      const float mv = b1 * m[q] + (1.f - b1) * gv;
+      const float vv = b2 * v[q] + (1.f - b2) * (gv * gv);
+      m[q] = mv;
+      v[q] = vv;
+      *wp = *wp - lr_t * mv / (sqrtf(vv) + eps);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+kge_status kge_apply(const kge_apply_desc* d, void* stream) {
+  if (!d) return fail(KGE_EINVAL, "null descriptor");
+  const kge_table& t = d->var;
+  if (!t.data || t.rows < 0 || t.cols <= 0 || t.ld < t.cols) return fail(KGE_EINVAL, "kge_apply: bad table");
+  if (d->optimizer != KGE_OPT_SGD && d->optimizer != KGE_OPT_ADAM)
+    return fail(KGE_EINVAL, "kge_apply: optimizer must be KGE_OPT_SGD or KGE_OPT_ADAM");
+  if (!d->grad || !d->norm2) return fail(KGE_EINVAL, "kge_apply: null grad / norm2");
+  if (!(d->clip_norm > 0.f)) return fail(KGE_EINVAL, "kge_apply: clip_norm must be > 0");
+  const bool adam = d->optimizer == KGE_OPT_ADAM;
+  double lr_t = 0.0;
+  if (adam) {
+    if (!d->m || !d->v) return fail(KGE_EINVAL, "kge_apply: Adam needs m and v slots");
+    if (d->iteration < 1) return fail(KGE_EINVAL, "kge_apply: Adam iteration must be >= 1");
+    const double t = (double)d->iteration;
+    lr_t = (double)d->lr * std::sqrt(1.0 - std::pow((double)d->beta_2, t)) / (1.0 - std::pow((double)d->beta_1, t));
+  }
+  const int64_t total = t.rows * t.cols;
+  if (total == 0) return KGE_OK;
+  const int64_t blocks = std::min<int64_t>(ceil_div(total, 256), 8192);
+  hipLaunchKernelGGL(apply_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, t.data, t.rows,
+                     (int32_t)t.cols, t.ld, d->grad, d->norm2, d->lr, d->clip_norm, adam ? 1 : 0, d->m, d->v,
+                     d->beta_1, d->beta_2, d->epsilon, (float)lr_t);
+  return hip_check("kge_apply");
+}
 
 int32_t kge_abi_version(void) { return KGE_ABI_VERSION; }
 
@@ -275,8 +334,13 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
 
   hipEvent_t const* ev = (hipEvent_t const*)d->prof_events;
   if (ev) (void)hipEventRecord(ev[0], st);
+  if (A.grad_mode) {
+    (void)hipMemsetAsync(d->grad_out[0], 0, (size_t)A.ent.rows * A.ent.cols * sizeof(float), st);
+    (void)hipMemsetAsync(d->grad_out[1], 0, (size_t)A.rel.rows * A.rel_gcols * sizeof(float), st);
+  }
   // _constraint_loss assigns before scoring (BaseModel.py:319)
-  const bool renorm = d->constraint && (d->model == KGE_MODEL_TRANSE || d->model == KGE_MODEL_DISTMULT);
+  const bool renorm = d->constraint && !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT) &&
+                      (d->model == KGE_MODEL_TRANSE || d->model == KGE_MODEL_DISTMULT);
   if (renorm) {
     const int64_t blocks = std::min<int64_t>(ceil_div(d->ent.rows, kWaves), 4096);
     hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, d->ent.data,

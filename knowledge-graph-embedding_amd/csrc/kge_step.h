@@ -14,6 +14,7 @@ struct StepArgs {
   bool given;
   bool pw;          // LpDistancePow
   bool rel_half;    // RotatE: relation row is the phase half-row
+  bool grad_mode;   // KGE_OPT_GRAD: write summed gradients, no update
   int64_t B;
   int32_t Keff;     // negatives per positive actually produced
   int32_t Kside;    // draws per side
@@ -39,6 +40,9 @@ struct StepArgs {
   float* part;
   uint64_t* sorted;
   int32_t* starts;
+  // KGE_OPT_GRAD outputs: dense [E, ent.cols] / [R, rel_gcols]
+  float* gent;
+  float* grel;
   // outputs
   float* loss_out;
   float* loss_accum;

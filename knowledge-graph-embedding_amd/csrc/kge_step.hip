@@ -506,6 +506,10 @@ __global__ __launch_bounds__(256) void update_kernel(StepArgs A) {
       }
     }
     if (!any) return;
+    if (A.grad_mode) {
+      store_rel_row<M::CPLX, VEC, NC>(acc, A.grel + r * (int64_t)A.rel_gcols, A.rel.cols);
+      return;
+    }
     float row[RV * NC];
     load_rel_row<M::CPLX, VEC, NC>(row, A.rel.row(r), A.rel.cols);
     const float sc = s_scale[1];
@@ -609,6 +613,12 @@ __global__ __launch_bounds__(256) void update_kernel(StepArgs A) {
         load_row(E, A.ent.row(e), A.ent.cols);
         acc.zero();
         for (int s = s0; s < s1; ++s) apply_entry(s_list[s], E, acc);
+        if (A.grad_mode) {
+          store_row(acc, A.gent + e * (int64_t)A.ent.cols, A.ent.cols);
+          ++seg;
+          s0 = s1;
+          continue;
+        }
         const float sc = s_scale[0];
 #pragma unroll
         for (int q = 0; q < VEC * NC; ++q) E.v[q] = E.v[q] + acc.v[q] * sc;
@@ -657,9 +667,10 @@ __global__ __launch_bounds__(256) void update_kernel(StepArgs A) {
         const int idx = (c * KGE_WAVE + lane) * VEC + k;
         float s = 0.f;
         for (int w = 0; w < W; ++w) s += red[w * FL + idx];
-        E.v[q] = E.v[q] + s * s_scale[0];
+        if (A.grad_mode) E.v[q] = s;
+        else E.v[q] = E.v[q] + s * s_scale[0];
       }
-      store_row(E, A.ent.row_w(e), A.ent.cols);
+      store_row(E, A.grad_mode ? A.gent + e * (int64_t)A.ent.cols : A.ent.row_w(e), A.ent.cols);
     }
     __syncthreads();
   }

@@ -296,9 +296,15 @@ def _constraint(model, W, L, X, cfg, batch_scale):
 
 def train_step(model, weights, pos, neg_ids, score=("lp", 2.0), loss=("hinge", 1.0), lr=0.01, constraint=True,
                constraint_weight=1.0, side="h+t", train=True, batch_scale=1.0, limit=None,
-               clip_norm=5.0, dtype=F64):
+               clip_norm=5.0, dtype=F64, optimizer="sgd", adam=(0.9, 0.999, 1e-7)):
     """One reference step with injected negatives. Returns dict with loss,
-    pos_score, neg_score, weights (numpy, updated) and norm2 per variable."""
+    pos_score, neg_score, weights (numpy, updated) and norm2 per variable.
+
+    optimizer "sgd": keras SGD (sparse ResourceScatterAdd of -lr * g).
+    optimizer "adam": the FIRST keras Adam step from zero slots (OptimizerV2,
+    TF 2.5): slices de-duplicated (summed per row), m = (1-b1) g,
+    v = (1-b2) g^2, var -= lr_t m / (sqrt(v) + eps) over every row,
+    lr_t = lr sqrt(1-b2) / (1-b1)."""
     W = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in weights.items()}
     names = list(W.keys())
     pos = np.asarray(pos, dtype=np.int64)
@@ -339,13 +345,26 @@ def train_step(model, weights, pos, neg_ids, score=("lp", 2.0), loss=("hinge", 1
                     l2 = torch.sum(tot * tot)
                     out["norm2"][n] = float(l2)
                     tot = tot * clip_norm / max(math.sqrt(float(l2)), clip_norm)
-                    w.add_(-lr * tot)
+                    if optimizer == "adam":
+                        _adam_first_step(w, tot, lr, *adam)
+                    else:
+                        w.add_(-lr * tot)
                 else:
                     idx = torch.cat([i for i, _ in sl])
                     vals = torch.cat([g for _, g in sl])
                     l2 = torch.sum(vals * vals)
                     out["norm2"][n] = float(l2)
                     vals = vals * clip_norm / max(math.sqrt(float(l2)), clip_norm)
-                    w.index_add_(0, idx, -lr * vals)
+                    if optimizer == "adam":
+                        _adam_first_step(w, torch.zeros_like(w).index_add_(0, idx, vals), lr, *adam)
+                    else:
+                        w.index_add_(0, idx, -lr * vals)
     out["weights"] = {k: v.detach().numpy() for k, v in W.items()}
     return out
+
+
+def _adam_first_step(w, g, lr, b1, b2, eps):
+    m = (1 - b1) * g
+    v = (1 - b2) * g * g
+    lr_t = lr * math.sqrt(1 - b2) / (1 - b1)
+    w.sub_(lr_t * m / (torch.sqrt(v) + eps))

@@ -1,0 +1,84 @@
+"""GPU: the reference's integration matrix (tests/test_integration.py:22-216)
+through KGEModel.train on cuda:0 -- built-in combinations run the fused HIP
+step (libkge_hip.so), the rest the plugin path on the device -- plus the
+golden toy-KG steps of tests/golden/step_golden.npz through kge_step."""
+
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.test_plugin_surface import MODELS, TRANSLATING, _losses, _samplers, _scores, build, toy
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(autouse=True)
+def _fused(monkeypatch, hiplib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("KGE_BACKEND", "fused")
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_integration_matrix_gpu(name, tmp_path):
+    train, val, md = toy()
+    scores = _scores(name) if name in TRANSLATING else [None]
+    for s in scores:
+        for l_ in _losses():
+            for sampler in _samplers(md):
+                for opt in ("SGD", "Adam"):
+                    m = build(name, s, l_, sampler)
+                    m.train(train_X=train, val_X=val, metadata=md, epochs=1, batch_size=4, optimizer=opt,
+                            seed=12345, log_path=str(tmp_path))
+                    assert np.isfinite(m.train_loss_history[0]) or type(l_).__name__ == "PairwiseLogisticLoss"
+                    r = m.evaluate(eval_X=val, corrupt_side="t")
+                    assert r["mean_rank"] >= 1
+
+
+def _golden_cases():
+    with open(os.path.join(GOLD, "step_golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("meta", _golden_cases(), ids=lambda m: "%s-%s-%s" % (m["model"], m["score"][0], m["loss"][0]))
+def test_step_golden_fused(meta):
+    """The committed golden step vectors (toy KG, injected negatives) through kge_step."""
+    from KGE import engine, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    z = np.load(os.path.join(GOLD, "step_golden.npz"))
+    tag = meta["tag"]
+    W = {k.split("/")[-1]: z[k] for k in z.files if k.startswith(tag + "/in/")}
+    sc = {"lp": score.LpDistance, "lppow": score.LpDistancePow}
+    s = score.Dot() if meta["score"][0] == "dot" else sc[meta["score"][0]](meta["score"][1])
+    lf = {"hinge": lambda a: loss.PairwiseHingeLoss(a[1]), "logistic": lambda a: loss.PairwiseLogisticLoss(),
+          "bce": lambda a: loss.BinaryCrossEntropyLoss(),
+          "sans": lambda a: loss.SelfAdversarialNegativeSamplingLoss(a[1], a[2]),
+          "sqerr": lambda a: loss.SquareErrorLoss()}[meta["loss"][0]](meta["loss"])
+    E = W["ent_emb"].shape[0]
+    m = build(meta["model"], s if meta["model"] not in ("DistMult", "RESCAL") else None, lf,
+              UniformStrategy(np.arange(E), seed=1))
+    if meta["model"] in ("TransR", "TransD"):
+        m.embedding_params = {"ent_embedding_size": meta["d"], "rel_embedding_size": meta["d"]}
+    else:
+        m.embedding_params = {"embedding_size": meta["d"]}
+    m.metadata = {"ind2ent": list(range(E)), "ind2rel": list(range(W[[k for k in W if k != "ent_emb"][0]].shape[0]))}
+    if meta["model"] == "RotatE":
+        m.limit = meta["limit"]
+    dev = torch.device("cuda", 0)
+    m.model_weights = {k: torch.tensor(v, dtype=torch.float32, device=dev) for k, v in W.items()}
+    reason = engine.fused_plan(m, optimizers.SGD(meta["lr"]))
+    if reason is not None:
+        pytest.skip("not fused in this build: %s" % reason)
+    step = engine.FusedStep(m)
+    pos = torch.tensor(z["pos"], device=dev)
+    neg = torch.tensor(z[tag + "/neg"], device=dev)
+    step(pos, True, optimizers.SGD(meta["lr"]), neg_ids=neg)
+    torch.cuda.synchronize()
+    step.check_status()
+    assert abs(float(step.loss_out) - float(z[tag + "/loss"])) <= 1e-5 * max(1.0, abs(float(z[tag + "/loss"])))
+    for k in W:
+        np.testing.assert_allclose(m.model_weights[k].cpu().numpy(), z["%s/out/%s" % (tag, k)], atol=1e-5, err_msg=k)

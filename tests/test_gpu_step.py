@@ -71,7 +71,7 @@ def _spec_loss(lf):
 
 
 def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, idx=torch.int64, train=True,
-             seed=11, constraint=True, typed=None, lr=0.05):
+             seed=11, constraint=True, typed=None, lr=0.05, opt="sgd"):
     from KGE import engine, optimizers
     from KGE.ns_strategy import TypedStrategy, UniformStrategy
     dev = _dev()
@@ -91,7 +91,8 @@ def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, id
     batch = torch.tensor(pos, device=dev, dtype=idx)
     plane = sampler.offset
     # sampled ids are also returned through a standalone call of the same planes
-    step(batch, train, optimizers.SGD(lr) if train else None, pos_score=ps, neg_score=ns)
+    o = (optimizers.SGD(lr) if opt == "sgd" else optimizers.Adam(lr)) if train else None
+    step(batch, train, o, pos_score=ps, neg_score=ns)
     torch.cuda.synchronize()
     step.check_status()
     i64 = idx == torch.int64
@@ -102,7 +103,7 @@ def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, id
     ref = orc.train_step(model_name, W, pos, neg, score=_spec_score(getattr(m, "score_fn", None))
                          if model_name != "DistMult" else ("dot", 0.0), loss=_spec_loss(loss_fn), lr=lr,
                          constraint=constraint if model_name != "RotatE" else False, side=side, train=train,
-                         limit=lim)
+                         limit=lim, optimizer=opt)
     got = {k: v.cpu().numpy() for k, v in m.model_weights.items()}
     return ref, got, float(step.loss_out.item()), ps.cpu().numpy(), ns.cpu().numpy(), step, neg
 
@@ -264,3 +265,51 @@ def test_fb15k237_bench_shape_properties(hiplib):
     assert math.isfinite(outs[0][0])
     assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
     assert bool(torch.isfinite(outs[0][1]).all()) and float(outs[0][3][0]) > 0
+
+
+@pytest.mark.parametrize("model_name", ["TransE", "DistMult", "RotatE"])
+def test_fused_adam_first_step(hiplib, model_name):
+    """kge_step(KGE_OPT_GRAD) + kge_apply(KGE_OPT_ADAM) == keras Adam (oracle)."""
+    from KGE import loss, score
+    sc = score.LpDistance(2) if model_name != "DistMult" else None
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, model_name, 32, 12, 6, "h+t", sc,
+                                          loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), opt="adam", lr=0.01)
+    check(ref, got, l_, ps, ns)
+
+
+def test_sharded_step_world1_rccl(hiplib):
+    """KGE/sharded.py on the RCCL backend (world size 1): shard, all-gather,
+    grad-mode kge_step, all-reduce, reduce-scatter, kge_apply == the oracle step."""
+    import socket
+    import torch.distributed as dist
+    from KGE import loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    from KGE.sharded import ShardedStep
+    dev = _dev()
+    s_ = socket.socket()
+    s_.bind(("127.0.0.1", 0))
+    port = s_.getsockname()[1]
+    s_.close()
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        rng = np.random.default_rng(3)
+        E, R, d, B, K = 37, 5, 64, 16, 8
+        W = _weights("TransE", E, R, d, rng)
+        pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+        m = _make("TransE", d, K, "h+t", score.LpDistance(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
+                  E, R, UniformStrategy(np.arange(E), seed=9))
+        m.model_weights = {k: torch.tensor(v, device=dev) for k, v in W.items()}
+        st = ShardedStep(m)
+        plane = m.ns_strategy.offset
+        lv = float(st(torch.tensor(pos, device=dev), True, optimizers.SGD(0.05)))
+        torch.cuda.synchronize()
+        st.check_status()
+        st.sync()
+        neg = orc.negatives(pos, K, "h+t", E, seed=9, plane=plane)
+        ref = orc.train_step("TransE", W, pos, neg, score=("lp", 2.0), loss=("sans", 3.0, 1.0), lr=0.05)
+        assert abs(lv - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"]))
+        for k, v in ref["weights"].items():
+            np.testing.assert_allclose(m.model_weights[k].cpu().numpy(), v, atol=TOL, err_msg=k)
+    finally:
+        dist.destroy_process_group()

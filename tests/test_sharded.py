@@ -1,0 +1,119 @@
+"""CPU (gloo, world size 2): the multi-GPU step's exchange logic
+(KGE/sharded.py) -- row-sharded entity table, all-gather, global-batch loss
+normalisation, reduce-scatter, global clip norm, sharded apply -- gives the
+single-device step on the concatenated batch. The local gradient phase runs
+the host restatement (KGE_BACKEND=eager); on GPUs it is kge_step."""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from oracle import kge_oracle as orc
+
+E, R, D, B, K = 13, 4, 8, 5, 4   # E odd: the last shard is padded
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _model(name, W, loss):
+    from KGE import loss as L
+    from KGE import score
+    from KGE.models.semantic_based.DistMult import DistMult
+    from KGE.models.translating_based.TransE import TransE
+    from KGE.ns_strategy import UniformStrategy
+    lf = {"sans": L.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), "hinge": L.PairwiseHingeLoss(1.0),
+          "bce": L.BinaryCrossEntropyLoss()}[loss]
+    if name == "TransE":
+        m = TransE({"embedding_size": D}, K, "h+t", score_fn=score.LpDistance(2), loss_fn=lf,
+                   ns_strategy=UniformStrategy(np.arange(E), seed=1), constraint=True)
+    else:
+        m = DistMult({"embedding_size": D}, K, "h+t", loss_fn=lf, ns_strategy=UniformStrategy(np.arange(E), seed=1),
+                     constraint=True, constraint_weight=0.1)
+    m.metadata = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
+    m.model_weights = {k: torch.tensor(v, dtype=torch.float32) for k, v in W.items()}
+    return m
+
+
+def _case(seed, name):
+    rng = np.random.default_rng(seed)
+    rk = "rel_emb" if name == "TransE" else "rel_inter"
+    W = {"ent_emb": rng.uniform(-0.5, 0.5, (E, D)), rk: rng.uniform(-0.5, 0.5, (R, D))}
+    pos = np.stack([rng.integers(0, E, 2 * B), rng.integers(0, R, 2 * B), rng.integers(0, E, 2 * B)], 1)
+    neg = rng.integers(0, E, 2 * B * K)
+    return W, pos, neg
+
+
+def _worker(rank, port, name, loss, opt, steps, out):
+    os.environ["KGE_BACKEND"] = "eager"
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=2)
+    from KGE import optimizers
+    from KGE.sharded import ShardedStep
+    W, pos, neg = _case(0, name)
+    m = _model(name, W, loss)
+    st = ShardedStep(m)
+    o = optimizers.SGD(0.05) if opt == "sgd" else optimizers.Adam(0.01)
+    for s in range(steps):
+        b = torch.tensor(pos[rank * B:(rank + 1) * B])
+        n = torch.tensor(neg[rank * B * K:(rank + 1) * B * K])
+        loss_v = float(st(b, True, o, neg_ids=n))
+    st.sync()
+    if rank == 0:
+        out.put(({k: v.detach().numpy().copy() for k, v in m.model_weights.items()}, loss_v))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(name, loss, opt, steps):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, port, name, loss, opt, steps, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = q.get(timeout=240)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("name,loss", [("TransE", "sans"), ("TransE", "hinge"), ("DistMult", "bce")])
+def test_sharded_sgd_equals_single_device_oracle(name, loss):
+    got, got_loss = _run(name, loss, "sgd", 1)
+    W, pos, neg = _case(0, name)
+    spec = {"sans": ("sans", 3.0, 1.0), "hinge": ("hinge", 1.0), "bce": ("bce",)}[loss]
+    sc = ("lp", 2.0) if name == "TransE" else ("dot", 0.0)
+    ref = orc.train_step(name, W, pos, neg, score=sc, loss=spec, lr=0.05, constraint=True,
+                         constraint_weight=0.1, side="h+t")
+    assert abs(got_loss - ref["loss"]) <= 1e-5 * max(1.0, abs(ref["loss"]))
+    for k, v in ref["weights"].items():
+        np.testing.assert_allclose(got[k], v, atol=2e-6, err_msg=k)
+
+
+def test_sharded_adam_equals_single_device_eager():
+    """Two Adam steps across 2 ranks == two steps of the single-process eager path at 2B."""
+    os.environ["KGE_BACKEND"] = "eager"
+    try:
+        from KGE import engine, optimizers
+        got, _ = _run("TransE", "sans", "adam", 2)
+        W, pos, neg = _case(0, "TransE")
+        m = _model("TransE", W, "sans")
+        o = optimizers.Adam(0.01)
+        negt = torch.tensor(orc.corrupt(pos, neg, K, "h+t"))
+        for _ in range(2):
+            engine.eager_step(m, torch.tensor(pos), True, o, neg=negt)
+    finally:
+        os.environ.pop("KGE_BACKEND", None)
+    for k, v in m.model_weights.items():
+        np.testing.assert_allclose(got[k], v.numpy(), atol=2e-6, err_msg=k)
