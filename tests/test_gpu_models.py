@@ -61,6 +61,7 @@ def test_step_golden_fused(meta):
     E = W["ent_emb"].shape[0]
     m = build(meta["model"], s if meta["model"] not in ("DistMult", "RESCAL") else None, lf,
               UniformStrategy(np.arange(E), seed=1))
+    m.negative_ratio = meta["K"]
     if meta["model"] in ("TransR", "TransD"):
         m.embedding_params = {"ent_embedding_size": meta["d"], "rel_embedding_size": meta["d"]}
     else:
