@@ -36,8 +36,7 @@ inline int64_t round_up(int64_t a, int64_t b) { return ceil_div(a, b) * b; }
 inline int next_pow2(int64_t x) { int p = 1; while (p < x) p <<= 1; return p; }
 inline bool aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
 
-constexpr int kWaves = 4;
-constexpr int kUCap = 4096;   // update kernel: LDS list capacity (entries)
+constexpr int kWaves = 4;      // constrain / sample / apply kernels: waves per workgroup
 
 struct Plan {
   StepArgs A;
@@ -45,7 +44,7 @@ struct Plan {
   int sk;
   uint64_t ws_bytes;
   // workspace offsets
-  uint64_t o_ids, o_coef, o_snap, o_gpos, o_part, o_sorted, o_starts;
+  uint64_t o_coef, o_snap, o_gpos, o_part, o_sorted, o_bmap;
 };
 
 int score_sk(int kind, float p) {
@@ -139,32 +138,38 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     return fail(KGE_EUNSUPPORTED, "row of %lld floats exceeds the fused kernel's %d", (long long)rowlen, 256 * vec);
   const int ncp = nc <= 1 ? 1 : nc <= 2 ? 2 : 4;
 
-  int nP = Keff >= 128 ? 1 : std::max(1, std::min(64, 256 / std::max(Keff, 1)));
-  nP = (int)std::max<int64_t>(1, std::min<int64_t>(nP, B / 256));
+  // score kernel: wpp waves per positive so that each wave holds <= ROWS
+  // sampled rows in registers; 8 / wpp positives per workgroup
+  const int ROWS = 32 / ncp;
+  int wpp = 1;
+  while (wpp < kStepWaves && (int64_t)wpp * ROWS < Keff) wpp <<= 1;
+  const int nP = kStepWaves / wpp;
+  const int SW = std::max<int>(1, (int)ceil_div(Keff, wpp));
   const int64_t nWG = std::max<int64_t>(1, ceil_div(B, nP));
-  const int64_t slotmax = (int64_t)nP * (Keff + 2);
-  if (slotmax > 65535) return fail(KGE_EUNSUPPORTED, "negative_ratio %d too large for one workgroup", K);
   if (nWG > 65535) return fail(KGE_EUNSUPPORTED, "batch %lld too large (max %d workgroups)", (long long)B, 65535);
-  const int sortpad = next_pow2(slotmax);
-  if (sortpad > 8192) return fail(KGE_EUNSUPPORTED, "negative_ratio %d too large (LDS sort)", K);
+  const int64_t slotmax = (int64_t)nP * (Keff + 3);
+  if (slotmax > 65535) return fail(KGE_EUNSUPPORTED, "negative_ratio %d too large for one workgroup", K);
 
+  // update kernel: destinations [0, E) entities and [E, E+R) relations in P
+  // buckets of bs, ~256 keys per bucket
   const int64_t E = d->ent.rows, R = d->rel.rows;
-  const int64_t T = B * (Keff + 2);
-  int64_t Pb = std::max<int64_t>(1, std::min<int64_t>({ceil_div(T, 256), E, 65535}));
-  const int64_t bs = ceil_div(E, Pb);
-  Pb = ceil_div(E, bs);
+  const int64_t ndest = E + R;
+  const int64_t T = B * (Keff + 3);
+  int64_t Pb = std::max<int64_t>(1, std::min<int64_t>({ceil_div(T, 256), ndest, (int64_t)kMaxBuckets}));
+  const int64_t bs = ceil_div(ndest, Pb);
+  Pb = ceil_div(ndest, bs);
 
   const int FL = 64 * vec * ncp;
-  const int Kpad = (int)round_up(Keff + 1, 4);
-  const int idpad = (int)round_up((int64_t)nP * Keff, 4);
+  const int Kp = (int)round_up(Keff + 1, 4);
+  const ScoreLds SL = score_lds(FL, nP, Kp, Keff, (int)slotmax, (int)Pb);
   P.G.vec = vec;
   P.G.nc = ncp;
   P.G.nWG = (int)nWG;
-  P.G.gridU = (int)(Pb + ceil_div(R, kWaves));
-  P.G.lds_score = (size_t)kWaves * 3 * FL * 4 + 4 * (size_t)Kpad * 4 + (size_t)idpad * 4 + 64 * 4 +
-                  (size_t)sortpad * 8 + (size_t)nP * 3 * 8;
-  P.G.lds_update = (size_t)kUCap * 8 + 264 * 4 + (size_t)kWaves * FL * 4;
-  if (P.G.lds_score > 160 * 1024) return fail(KGE_EUNSUPPORTED, "LDS budget exceeded");
+  P.G.gridU = (int)Pb;
+  P.G.lds_score = (size_t)SL.total;
+  P.G.lds_update = (size_t)kUCap * 8 + (size_t)(kUCap + 4) * 4 + (size_t)kStepWaves * FL * 4;
+  if (P.G.lds_score > 160 * 1024 || P.G.lds_update > 160 * 1024)
+    return fail(KGE_EUNSUPPORTED, "LDS budget exceeded (score %zu, update %zu bytes)", P.G.lds_score, P.G.lds_update);
   P.sk = score_sk(d->score_kind, p);
 
   A.ent = TabView{d->ent.data, d->ent.ld, (int32_t)entc, E};
@@ -195,15 +200,14 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.rel_reg = (model == KGE_MODEL_DISTMULT && d->constraint) ? d->constraint_weight : 0.f;
   A.lr = d->lr;
   A.clip_norm = d->clip_norm;
+  A.wpp = wpp;
   A.nP = nP;
+  A.SW = SW;
   A.nWG = (int32_t)nWG;
-  A.Kpad = Kpad;
-  A.idpad = idpad;
-  A.sortpad = sortpad;
+  A.Kp = Kp;
   A.slotmax = (int32_t)slotmax;
   A.P = (int32_t)Pb;
   A.bs = bs;
-  A.ucap = kUCap;
   A.snap_cols = (int32_t)entc;
   A.gcols = (int32_t)rowlen;
   A.rel_gcols = (int32_t)relc;
@@ -216,13 +220,13 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
 
   uint64_t off = 0;
   auto take = [&](uint64_t bytes) { const uint64_t o = off; off += round_up((int64_t)bytes, 256); return o; };
-  P.o_ids = take((uint64_t)B * Keff * 4);
+  const int nsnap = model == KGE_MODEL_ROTATE ? 3 : 2;
   P.o_coef = take((uint64_t)B * Keff * 8);
-  P.o_snap = take((uint64_t)B * 3 * entc * 4);
+  P.o_snap = take((uint64_t)B * nsnap * entc * 4);
   P.o_gpos = take((uint64_t)B * 3 * rowlen * 4);
   P.o_part = take((uint64_t)nWG * 8 * 4);
   P.o_sorted = take((uint64_t)nWG * slotmax * 8);
-  P.o_starts = take((uint64_t)nWG * (Pb + 1) * 4);
+  P.o_bmap = take((uint64_t)Pb * nWG * 4);
   P.ws_bytes = std::max<uint64_t>(off, 256);
   return KGE_OK;
 }
@@ -324,13 +328,12 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   StepArgs& A = P.A;
   unsigned char* ws = (unsigned char*)d->workspace;
-  A.ids = (int32_t*)(ws + P.o_ids);
   A.coef = (float2*)(ws + P.o_coef);
   A.snap = (float*)(ws + P.o_snap);
   A.gpos = (float*)(ws + P.o_gpos);
   A.part = (float*)(ws + P.o_part);
   A.sorted = (uint64_t*)(ws + P.o_sorted);
-  A.starts = (int32_t*)(ws + P.o_starts);
+  A.bmap = (uint32_t*)(ws + P.o_bmap);
 
   hipEvent_t const* ev = (hipEvent_t const*)d->prof_events;
   if (ev) (void)hipEventRecord(ev[0], st);

@@ -165,18 +165,27 @@ struct MP {
   float limit;   // RotatE phase range (RotatE.py:93)
 };
 
-// Snapshot rows written per positive by the score kernel and read back by
-// the update kernel (the positive's context, frozen before any update).
-// All three rows have `snap_cols` floats.
+// Context rows ("snap") written per positive by the score kernel and read
+// back by the update kernel: everything a sampled row's gradient needs
+// besides the row itself and its coefficient, frozen before any update.
+// NSNAP rows of `cols` floats each. A negative's update-side context is ONE
+// row for TransE / DistMult and at most two for RotatE.
 
 // ======================================================================
 // TransE: s(h + r, t)      (TransE.py:149-155)
+//   positive      a = (h + r) - t            (the reference's op order)
+//   t-corrupted   a = X - e,   X = h + r     (snap row 0)
+//   h-corrupted   a = e + D,   D = r - t     (snap row 1)
+// The update kernel rebuilds `a` from the same snap rows, so both kernels
+// hold identical bits (the p = inf arg-max test depends on it).
 // ======================================================================
 template <int VEC, int NC, int SK>
 struct TransE {
   static constexpr bool CPLX = false;
+  static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
-  struct Ctx { F X, R, T; };   // X = h + r
+  struct Ctx { F X, R, T, D; };
+  struct ECtx { F c0; };
 
   __device__ static void load_ctx(Ctx& c, const TabView& ent, const TabView& rel, int64_t h,
                                   int64_t r, int64_t t, const MP&) {
@@ -185,19 +194,22 @@ struct TransE {
     load_row(c.R, rel.row(r), rel.cols);
     load_row(c.T, ent.row(t), ent.cols);
 #pragma unroll
-    for (int i = 0; i < VEC * NC; ++i) c.X.v[i] = H.v[i] + c.R.v[i];
+    for (int i = 0; i < VEC * NC; ++i) {
+      c.X.v[i] = H.v[i] + c.R.v[i];
+      c.D.v[i] = c.R.v[i] - c.T.v[i];
+    }
   }
-  // a/b for the score (Lp: a = x - y; Dot: a = x, b = y)
   __device__ static void fwd(const Ctx& c, int kind, const F& E, F& a, F& b) {
 #pragma unroll
     for (int i = 0; i < VEC * NC; ++i) {
-      const float x = kind == KIND_HC ? E.v[i] + c.R.v[i] : c.X.v[i];
-      const float y = kind == KIND_TC ? E.v[i] : c.T.v[i];
-      if (SK == SK_DOT) { a.v[i] = x; b.v[i] = y; }
-      else a.v[i] = x - y;
+      if (SK == SK_DOT) {
+        a.v[i] = kind == KIND_HC ? E.v[i] + c.R.v[i] : c.X.v[i];
+        b.v[i] = kind == KIND_TC ? E.v[i] : c.T.v[i];
+      } else {
+        a.v[i] = kind == KIND_HC ? E.v[i] + c.D.v[i] : c.X.v[i] - (kind == KIND_TC ? E.v[i] : c.T.v[i]);
+      }
     }
   }
-  // gradients wrt x and y from a/b
   __device__ static void grad_xy(const F& a, const F& b, float alpha, float M, F& gx, F& gy) {
     if (SK == SK_DOT) {
 #pragma unroll
@@ -208,8 +220,6 @@ struct TransE {
       for (int i = 0; i < VEC * NC; ++i) gy.v[i] = -gx.v[i];
     }
   }
-  // accumulate the fixed rows (H: accH, R: accR, T: accT) and the per-variable
-  // sum of squared IndexedSlices values (norm[0] ent_emb, norm[1] rel_emb).
   __device__ static void bwd(const Ctx& c, int kind, const F& E, const F& a, const F& b,
                              float alpha, float M, F& accH, F& accR, F& accT, float* nrm,
                              const MP&) {
@@ -222,32 +232,49 @@ struct TransE {
     if (kind != KIND_HC) add_to(accH, gx);
     if (kind != KIND_TC) add_to(accT, gy);
   }
-  __device__ static void write_snap(const Ctx& c, float* s0, float* s1, float* s2, int cols) {
-    store_row(c.X, s0, cols);
-    store_row(c.R, s1, cols);
-    store_row(c.T, s2, cols);
+  __device__ static void write_snap(const Ctx& c, float* sb, int cols) {
+    store_row(c.X, sb, cols);
+    if (SK == SK_DOT) {   // Dot: h-corrupted needs r and t separately -> keep r + t? use D slot for t
+      store_row(c.T, sb + cols, cols);
+    } else {
+      store_row(c.D, sb + cols, cols);
+    }
   }
-  // update-kernel side: gradient of a negative wrt its sampled entity row E
-  __device__ static void grad_entity(const float* s0, const float* s1, const float* s2, int cols,
-                                     int kind, const F& E, float alpha, float M, F& gE) {
-    Ctx c;
-    if (kind == KIND_TC) load_row(c.X, s0, cols);
-    else { load_row(c.R, s1, cols); load_row(c.T, s2, cols); }
-    F a, b, gx, gy;
-    fwd(c, kind, E, a, b);
-    grad_xy(a, b, alpha, M, gx, gy);
-    gE = kind == KIND_HC ? gx : gy;
+  __device__ static void load_ectx(const float* sb, int cols, int kind, ECtx& ec) {
+    load_row(ec.c0, sb + (kind == KIND_TC ? 0 : cols), cols);
+  }
+  // gradient of a negative wrt its sampled entity row E
+  __device__ static void grad_entity(const ECtx& ec, int kind, const F& E, float alpha, float M, F& gE) {
+    if (SK == SK_DOT) {
+      // TC: d/dE (X . E) = alpha X ; HC: d/dE ((E + r) . t) = alpha t
+#pragma unroll
+      for (int i = 0; i < VEC * NC; ++i) gE.v[i] = alpha * ec.c0.v[i];
+      return;
+    }
+    F a, g;
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) a.v[i] = kind == KIND_HC ? E.v[i] + ec.c0.v[i] : ec.c0.v[i] - E.v[i];
+    score_grad<SK, false>(a, alpha, M, g);
+    if (kind == KIND_HC) gE = g;
+    else {
+#pragma unroll
+      for (int i = 0; i < VEC * NC; ++i) gE.v[i] = -g.v[i];
+    }
   }
 };
 
 // ======================================================================
 // DistMult: sum(h * r * t)     (DistMult.py:140-146); score_fn not used
+//   positive / t-corrupted: a = h*r (snap row 0), b = t-side row
+//   h-corrupted:            a = e,   b = t*r (snap row 1)
 // ======================================================================
 template <int VEC, int NC, int SK_UNUSED>
 struct DistMult {
   static constexpr bool CPLX = false;
+  static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
-  struct Ctx { F H, R, T, HR; };
+  struct Ctx { F H, R, T, HR, TR; };
+  struct ECtx { F c0; };
 
   __device__ static void load_ctx(Ctx& c, const TabView& ent, const TabView& rel, int64_t h,
                                   int64_t r, int64_t t, const MP&) {
@@ -255,14 +282,16 @@ struct DistMult {
     load_row(c.R, rel.row(r), rel.cols);
     load_row(c.T, ent.row(t), ent.cols);
 #pragma unroll
-    for (int i = 0; i < VEC * NC; ++i) c.HR.v[i] = c.H.v[i] * c.R.v[i];
+    for (int i = 0; i < VEC * NC; ++i) {
+      c.HR.v[i] = c.H.v[i] * c.R.v[i];
+      c.TR.v[i] = c.T.v[i] * c.R.v[i];
+    }
   }
-  // a = h*r, b = t   (TF evaluates (h * r) * t)
   __device__ static void fwd(const Ctx& c, int kind, const F& E, F& a, F& b) {
 #pragma unroll
     for (int i = 0; i < VEC * NC; ++i) {
-      a.v[i] = kind == KIND_HC ? E.v[i] * c.R.v[i] : c.HR.v[i];
-      b.v[i] = kind == KIND_TC ? E.v[i] : c.T.v[i];
+      a.v[i] = kind == KIND_HC ? E.v[i] : c.HR.v[i];
+      b.v[i] = kind == KIND_HC ? c.TR.v[i] : (kind == KIND_TC ? E.v[i] : c.T.v[i]);
     }
   }
   __device__ static void bwd(const Ctx& c, int kind, const F& E, const F& a, const F& b,
@@ -270,12 +299,12 @@ struct DistMult {
                              const MP&) {
     F gH, gR, gT;
     const F& Hv = kind == KIND_HC ? E : c.H;
+    const F& Tv = kind == KIND_TC ? E : c.T;
 #pragma unroll
     for (int i = 0; i < VEC * NC; ++i) {
-      const float ga = alpha * b.v[i];   // d/d(h*r)
-      gT.v[i] = alpha * a.v[i];
-      gH.v[i] = ga * c.R.v[i];
-      gR.v[i] = ga * Hv.v[i];
+      gH.v[i] = kind == KIND_HC ? alpha * c.TR.v[i] : (alpha * Tv.v[i]) * c.R.v[i];
+      gR.v[i] = (alpha * Tv.v[i]) * Hv.v[i];
+      gT.v[i] = kind == KIND_HC ? (alpha * E.v[i]) * c.R.v[i] : alpha * c.HR.v[i];
     }
     nrm[0] += sq_partial(gH) + sq_partial(gT);
     nrm[1] += sq_partial(gR);
@@ -283,25 +312,16 @@ struct DistMult {
     if (kind != KIND_HC) add_to(accH, gH);
     if (kind != KIND_TC) add_to(accT, gT);
   }
-  __device__ static void write_snap(const Ctx& c, float* s0, float* s1, float* s2, int cols) {
-    store_row(c.HR, s0, cols);
-    store_row(c.R, s1, cols);
-    store_row(c.T, s2, cols);
+  __device__ static void write_snap(const Ctx& c, float* sb, int cols) {
+    store_row(c.HR, sb, cols);
+    store_row(c.TR, sb + cols, cols);
   }
-  __device__ static void grad_entity(const float* s0, const float* s1, const float* s2, int cols,
-                                     int kind, const F& E, float alpha, float M, F& gE) {
-    if (kind == KIND_TC) {   // d/dt = c * (h*r)
-      F HR;
-      load_row(HR, s0, cols);
+  __device__ static void load_ectx(const float* sb, int cols, int kind, ECtx& ec) {
+    load_row(ec.c0, sb + (kind == KIND_TC ? 0 : cols), cols);
+  }
+  __device__ static void grad_entity(const ECtx& ec, int kind, const F& E, float alpha, float M, F& gE) {
 #pragma unroll
-      for (int i = 0; i < VEC * NC; ++i) gE.v[i] = alpha * HR.v[i];
-    } else {                 // d/dh = (c * t) * r
-      F R, T;
-      load_row(R, s1, cols);
-      load_row(T, s2, cols);
-#pragma unroll
-      for (int i = 0; i < VEC * NC; ++i) gE.v[i] = (alpha * T.v[i]) * R.v[i];
-    }
+    for (int i = 0; i < VEC * NC; ++i) gE.v[i] = alpha * ec.c0.v[i];
   }
 };
 
@@ -309,13 +329,16 @@ struct DistMult {
 // RotatE: s(h o e^{i theta}, t), theta = r / limit * pi   (RotatE.py:148-165)
 // ent rows are [d, 2] (re, im interleaved) -> 2d floats; rel rows d phases.
 // VEC must be 2 or 4 (complex pairs stay inside one lane).
+// snap rows: 0 = X = h o w, 1 = w = (cos, sin), 2 = t.
 // ======================================================================
 template <int VEC, int NC, int SK>
 struct RotatE {
   static constexpr bool CPLX = true;
+  static constexpr int NSNAP = 3;
   static constexpr int HV = VEC / 2;
   using F = Frag<VEC, NC>;
   struct Ctx { F H, X, CS, T; };   // CS = (cos, sin) interleaved, X = H o CS
+  struct ECtx { F c0, c1; };
   __device__ static void load_ctx(Ctx& c, const TabView& ent, const TabView& rel, int64_t h,
                                   int64_t r, int64_t t, const MP& mp) {
     const float limit = mp.limit;
@@ -375,32 +398,36 @@ struct RotatE {
     if (kind != KIND_HC) add_to(accH, gH);
     if (kind != KIND_TC) sub_to(accT, gx);
   }
-  __device__ static void write_snap(const Ctx& c, float* s0, float* s1, float* s2, int cols) {
-    store_row(c.X, s0, cols);
-    store_row(c.CS, s1, cols);
-    store_row(c.T, s2, cols);
+  __device__ static void write_snap(const Ctx& c, float* sb, int cols) {
+    store_row(c.X, sb, cols);
+    store_row(c.CS, sb + cols, cols);
+    store_row(c.T, sb + 2 * cols, cols);
   }
-  __device__ static void grad_entity(const float* s0, const float* s1, const float* s2, int cols,
-                                     int kind, const F& E, float alpha, float M, F& gE) {
+  __device__ static void load_ectx(const float* sb, int cols, int kind, ECtx& ec) {
     if (kind == KIND_TC) {
-      F X, a, g;
-      load_row(X, s0, cols);
+      load_row(ec.c0, sb, cols);
+    } else {
+      load_row(ec.c0, sb + cols, cols);
+      load_row(ec.c1, sb + 2 * cols, cols);
+    }
+  }
+  __device__ static void grad_entity(const ECtx& ec, int kind, const F& E, float alpha, float M, F& gE) {
+    if (kind == KIND_TC) {
+      F a, g;
 #pragma unroll
-      for (int i = 0; i < VEC * NC; ++i) a.v[i] = X.v[i] - E.v[i];
+      for (int i = 0; i < VEC * NC; ++i) a.v[i] = ec.c0.v[i] - E.v[i];
       score_grad<SK, true>(a, alpha, M, g);
 #pragma unroll
       for (int i = 0; i < VEC * NC; ++i) gE.v[i] = -g.v[i];
     } else {
-      F CS, T, x, a, g;
-      load_row(CS, s1, cols);
-      load_row(T, s2, cols);
-      cmul(E, CS, x);
+      F x, a, g;
+      cmul(E, ec.c0, x);
 #pragma unroll
-      for (int i = 0; i < VEC * NC; ++i) a.v[i] = x.v[i] - T.v[i];
+      for (int i = 0; i < VEC * NC; ++i) a.v[i] = x.v[i] - ec.c1.v[i];
       score_grad<SK, true>(a, alpha, M, g);
 #pragma unroll
       for (int i = 0; i < VEC * NC; i += 2) {
-        const float co = CS.v[i], si = CS.v[i + 1];
+        const float co = ec.c0.v[i], si = ec.c0.v[i + 1];
         gE.v[i] = g.v[i] * co + g.v[i + 1] * si;
         gE.v[i + 1] = g.v[i + 1] * co - g.v[i] * si;
       }
