@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
 echo "pytest_gpu exit $?" | tee -a "$OUT/status.txt"
 tail -5 "$OUT/pytest_gpu.log"
 grep -q -E "(Fatal|core dumped|Aborted|Segmentation)" "$OUT/pytest_gpu.log" && exit 3
