@@ -14,7 +14,10 @@
  *    in signatures; streams are passed as `void*` (a hipStream_t, NULL = the
  *    legacy default stream).
  *  - The library never allocates device memory: the caller passes a
- *    workspace of at least kge_step_workspace_bytes() bytes.
+ *    workspace of at least kge_step_workspace_bytes() bytes, ZERO-FILLED when
+ *    it is allocated (a fresh workspace must be zeroed once). Between calls it
+ *    holds only zeros again: the step's tickets and per-destination counters
+ *    reset themselves. One workspace serves one stream at a time.
  *  - Calls are stream-ordered, re-entrant and never throw. They return a
  *    kge_status; kge_last_error() gives a thread-local message.
  *  - Device-side range violations (entity / relation ids out of range) are
@@ -97,8 +100,10 @@ enum { KGE_OPT_NONE = 0, KGE_OPT_SGD = 1, KGE_OPT_GRAD = 2, KGE_OPT_ADAM = 3 };
 
 /* kge_step_desc.flags */
 enum {
-  KGE_FLAG_NO_TABLE_CONSTRAINT = 1  /* caller already applied the full-table
+  KGE_FLAG_NO_TABLE_CONSTRAINT = 1, /* caller already applied the full-table
                                        _constraint_loss assigns (e.g. on its shard) */
+  KGE_FLAG_DEBUG_LIST_CAP = 2       /* test hook: 4-entry destination lists, so the
+                                       update kernel's overflow path runs */
 };
 
 typedef struct kge_table {
@@ -196,7 +201,7 @@ typedef struct kge_step_desc {
   float* norm2_out;           /* [4] per-variable gradient norm^2 (nullable)    */
   int32_t* status;            /* device status word (nullable)                  */
 
-  void* workspace;
+  void* workspace;            /* zero-filled once at allocation (see the ABI rules) */
   uint64_t workspace_bytes;
   void* const* prof_events;   /* optional: 4 hipEvent_t recorded before K0, KS,
                                  KU and after KU (kernel timing; nullable)      */

@@ -231,7 +231,9 @@ class FusedStep:
             if need == 0:   # invalid descriptor: kge_step re-validates and reports the status
                 _hip.check(self.lib.kge_step(d, _hip.stream_handle(self.device)), "kge_step")
             if self.workspace.numel() < need:
-                self.workspace = torch.empty(need, dtype=torch.uint8, device=self.device)
+                # zero-filled once: the step's tickets / destination counters
+                # live in the workspace and reset themselves between calls
+                self.workspace = torch.zeros(need, dtype=torch.uint8, device=self.device)
             d.workspace = self.workspace.data_ptr()
             d.workspace_bytes = self.workspace.numel()
             self._cache = (key, d)

@@ -44,7 +44,7 @@ struct Plan {
   int sk;
   uint64_t ws_bytes;
   // workspace offsets
-  uint64_t o_coef, o_snap, o_gpos, o_part, o_sorted, o_bmap;
+  uint64_t o_ctl, o_cnt, o_coef, o_snap, o_gpos, o_part, o_list, o_ovf;
 };
 
 int score_sk(int kind, float p) {
@@ -138,38 +138,35 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     return fail(KGE_EUNSUPPORTED, "row of %lld floats exceeds the fused kernel's %d", (long long)rowlen, 256 * vec);
   const int ncp = nc <= 1 ? 1 : nc <= 2 ? 2 : 4;
 
-  // score kernel: wpp waves per positive so that each wave holds <= ROWS
-  // sampled rows in registers; 8 / wpp positives per workgroup
-  const int ROWS = 32 / ncp;
+  // score kernel: wpp waves per positive so that a wave streams <= 64 slots;
+  // 8 / wpp positives per workgroup
   int wpp = 1;
-  while (wpp < kStepWaves && (int64_t)wpp * ROWS < Keff) wpp <<= 1;
+  while (wpp < kMaxWpp && (int64_t)wpp * 64 < Keff) wpp <<= 1;
   const int nP = kStepWaves / wpp;
   const int SW = std::max<int>(1, (int)ceil_div(Keff, wpp));
   const int64_t nWG = std::max<int64_t>(1, ceil_div(B, nP));
-  if (nWG > 65535) return fail(KGE_EUNSUPPORTED, "batch %lld too large (max %d workgroups)", (long long)B, 65535);
-  const int64_t slotmax = (int64_t)nP * (Keff + 3);
-  if (slotmax > 65535) return fail(KGE_EUNSUPPORTED, "negative_ratio %d too large for one workgroup", K);
-
-  // update kernel: destinations [0, E) entities and [E, E+R) relations in P
-  // buckets of bs, ~256 keys per bucket
+  if (nWG > 0x7fffffff) return fail(KGE_EUNSUPPORTED, "batch %lld too large", (long long)B);
+  // destination keys: codes i*Keff + j (negatives), B*Keff + 3i + c (positive rows)
   const int64_t E = d->ent.rows, R = d->rel.rows;
   const int64_t ndest = E + R;
   const int64_t T = B * (Keff + 3);
-  int64_t Pb = std::max<int64_t>(1, std::min<int64_t>({ceil_div(T, 256), ndest, (int64_t)kMaxBuckets}));
-  const int64_t bs = ceil_div(ndest, Pb);
-  Pb = ceil_div(ndest, bs);
+  if (T >= (int64_t)0xFFFFFFFF) return fail(KGE_EUNSUPPORTED, "batch * (negative_ratio + 3) exceeds 2^32 keys");
+  // per-destination list capacity: ~4x the mean load, 64..256 entries (the
+  // update kernel orders up to 256 in registers; longer lists overflow)
+  int64_t cap = 64;
+  while (cap < 256 && cap < 4 * ceil_div(T, ndest)) cap <<= 1;
+  while (cap > 16 && ndest * cap * 4 > ((int64_t)1 << 30)) cap >>= 1;
+  if (d->flags & KGE_FLAG_DEBUG_LIST_CAP) cap = 4;   // test hook: exercise the overflow path
 
   const int FL = 64 * vec * ncp;
-  const int Kp = (int)round_up(Keff + 1, 4);
-  const ScoreLds SL = score_lds(FL, nP, Kp, Keff, (int)slotmax, (int)Pb);
+  const ScoreLds SL = score_lds(FL, nP, Keff);
   P.G.vec = vec;
   P.G.nc = ncp;
   P.G.nWG = (int)nWG;
-  P.G.gridU = (int)Pb;
+  P.G.gridU = (int)ceil_div(ndest, kUpdWaves);
   P.G.lds_score = (size_t)SL.total;
-  P.G.lds_update = (size_t)kUCap * 8 + (size_t)(kUCap + 4) * 4 + (size_t)kStepWaves * FL * 4;
-  if (P.G.lds_score > 160 * 1024 || P.G.lds_update > 160 * 1024)
-    return fail(KGE_EUNSUPPORTED, "LDS budget exceeded (score %zu, update %zu bytes)", P.G.lds_score, P.G.lds_update);
+  if (P.G.lds_score > 160 * 1024)
+    return fail(KGE_EUNSUPPORTED, "LDS budget exceeded (score kernel %zu bytes)", P.G.lds_score);
   P.sk = score_sk(d->score_kind, p);
 
   A.ent = TabView{d->ent.data, d->ent.ld, (int32_t)entc, E};
@@ -204,10 +201,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.nP = nP;
   A.SW = SW;
   A.nWG = (int32_t)nWG;
-  A.Kp = Kp;
-  A.slotmax = (int32_t)slotmax;
-  A.P = (int32_t)Pb;
-  A.bs = bs;
+  A.cap = (int32_t)cap;
+  A.nkeyneg = (uint32_t)(B * Keff);
   A.snap_cols = (int32_t)entc;
   A.gcols = (int32_t)rowlen;
   A.rel_gcols = (int32_t)relc;
@@ -221,12 +216,15 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   uint64_t off = 0;
   auto take = [&](uint64_t bytes) { const uint64_t o = off; off += round_up((int64_t)bytes, 256); return o; };
   const int nsnap = model == KGE_MODEL_ROTATE ? 3 : 2;
+  // zero-state words first: control block, per-destination counters
+  P.o_ctl = take(sizeof(StepCtl));
+  P.o_cnt = take((uint64_t)ndest * 4);
   P.o_coef = take((uint64_t)B * Keff * 8);
   P.o_snap = take((uint64_t)B * nsnap * entc * 4);
   P.o_gpos = take((uint64_t)B * 3 * rowlen * 4);
   P.o_part = take((uint64_t)nWG * 8 * 4);
-  P.o_sorted = take((uint64_t)nWG * slotmax * 8);
-  P.o_bmap = take((uint64_t)Pb * nWG * 4);
+  P.o_list = take((uint64_t)ndest * cap * 4);
+  P.o_ovf = take((uint64_t)T * 8);
   P.ws_bytes = std::max<uint64_t>(off, 256);
   return KGE_OK;
 }
@@ -328,12 +326,14 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   StepArgs& A = P.A;
   unsigned char* ws = (unsigned char*)d->workspace;
+  A.ctl = (StepCtl*)(ws + P.o_ctl);
+  A.cnt = (uint32_t*)(ws + P.o_cnt);
   A.coef = (float2*)(ws + P.o_coef);
   A.snap = (float*)(ws + P.o_snap);
   A.gpos = (float*)(ws + P.o_gpos);
   A.part = (float*)(ws + P.o_part);
-  A.sorted = (uint64_t*)(ws + P.o_sorted);
-  A.bmap = (uint32_t*)(ws + P.o_bmap);
+  A.list = (uint32_t*)(ws + P.o_list);
+  A.ovf = (uint64_t*)(ws + P.o_ovf);
 
   hipEvent_t const* ev = (hipEvent_t const*)d->prof_events;
   if (ev) (void)hipEventRecord(ev[0], st);

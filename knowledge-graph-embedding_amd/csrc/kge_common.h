@@ -108,7 +108,9 @@ __device__ __forceinline__ int64_t sample_entity(const SamplerView& s, uint64_t 
 
 // ---------------------------------------------------------------- waves
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (KGE_WAVE - 1); }
-__device__ __forceinline__ int wave_id() { return threadIdx.x / KGE_WAVE; }
+// wave index as a scalar (SGPR): everything derived from it stays wave-uniform,
+// so per-wave bounds compile to scalar branches, not exec-mask divergence
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x / KGE_WAVE); }
 
 __device__ __forceinline__ float wave_sum(float x) {
 #pragma unroll
@@ -135,21 +137,26 @@ struct Frag {
 template <int VEC>
 __device__ __forceinline__ int frag_elem(int c, int q) { return (c * KGE_WAVE + lane_id()) * VEC + q; }
 
+// Branch-free: lanes past the row's end load its first element group (same
+// cache lines, no extra traffic) and zero the value, so a row load is one
+// vector-memory instruction per chunk with no exec-mask branches. cols >= VEC.
 template <int VEC, int NC>
 __device__ __forceinline__ void load_row(Frag<VEC, NC>& f, const float* __restrict__ row, int cols) {
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int e0 = (c * KGE_WAVE + lane_id()) * VEC;
+    const bool in = e0 < cols;
+    const int e = in ? e0 : 0;
     if (VEC == 4) {
-      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e0 < cols) x = *reinterpret_cast<const float4*>(row + e0);
-      f.v[c * 4 + 0] = x.x; f.v[c * 4 + 1] = x.y; f.v[c * 4 + 2] = x.z; f.v[c * 4 + 3] = x.w;
+      const float4 x = *reinterpret_cast<const float4*>(row + e);
+      f.v[c * 4 + 0] = in ? x.x : 0.f; f.v[c * 4 + 1] = in ? x.y : 0.f;
+      f.v[c * 4 + 2] = in ? x.z : 0.f; f.v[c * 4 + 3] = in ? x.w : 0.f;
     } else if (VEC == 2) {
-      float2 x = make_float2(0.f, 0.f);
-      if (e0 < cols) x = *reinterpret_cast<const float2*>(row + e0);
-      f.v[c * 2 + 0] = x.x; f.v[c * 2 + 1] = x.y;
+      const float2 x = *reinterpret_cast<const float2*>(row + e);
+      f.v[c * 2 + 0] = in ? x.x : 0.f; f.v[c * 2 + 1] = in ? x.y : 0.f;
     } else {
-      f.v[c] = e0 < cols ? row[e0] : 0.f;
+      const float x = row[e];
+      f.v[c] = in ? x : 0.f;
     }
   }
 }
@@ -203,6 +210,24 @@ __device__ __forceinline__ void store_row_half(const float (&h)[(VEC / 2 > 0 ? V
     else row[e0] = h[c];
   }
 }
+
+// Phase profiling (profiling builds only, -DKGE_PHASE_PROF): thread 0 of each
+// workgroup adds the wall-clock ticks of each phase to a device counter.
+#ifdef KGE_PHASE_PROF
+extern __device__ unsigned long long g_kge_prof[64];
+#define KGE_PROF_INIT() unsigned long long kge_prof_t_ = threadIdx.x == 0 ? wall_clock64() : 0ull
+#define KGE_PROF(k)                                                   \
+  do {                                                                \
+    if (threadIdx.x == 0) {                                           \
+      const unsigned long long kge_prof_n_ = wall_clock64();          \
+      atomicAdd(&g_kge_prof[(k)], kge_prof_n_ - kge_prof_t_);         \
+      kge_prof_t_ = kge_prof_n_;                                      \
+    }                                                                 \
+  } while (0)
+#else
+#define KGE_PROF_INIT() do {} while (0)
+#define KGE_PROF(k) do {} while (0)
+#endif
 
 __device__ __forceinline__ void set_status(int32_t* status, int code) {
   if (status) atomicCAS(status, 0, code);

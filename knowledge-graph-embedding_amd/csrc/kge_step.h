@@ -5,10 +5,25 @@
 
 namespace kge {
 
-constexpr int kStepWaves = 8;      // waves per workgroup, score and update kernels
+constexpr int kStepWaves = 8;      // waves per score workgroup
 constexpr int kStepThreads = kStepWaves * KGE_WAVE;
-constexpr int kUCap = 4096;        // update kernel: LDS list capacity (entries)
-constexpr int kMaxBuckets = 8192;  // score kernel: LDS bucket counters
+constexpr int kUpdWaves = 4;       // waves per update workgroup (one destination row per wave)
+constexpr int kUpdThreads = kUpdWaves * KGE_WAVE;
+constexpr int kMaxWpp = 8;         // waves per positive, at most
+constexpr int kMergeStride = 32;   // floats of per-positive merge state in the score kernel's LDS
+
+// Control block at the head of the workspace. The caller zero-fills the
+// workspace once when it allocates it; every kernel that uses a word puts it
+// back to zero before the step ends (self-resetting tickets and counters).
+struct StepCtl {
+  uint32_t score_ticket;   // score workgroups done (the last one reduces the partials)
+  uint32_t ovf_count;      // overflow-list appends of the running score kernel
+  uint32_t ovf_len;        // overflow-list length for the update kernel (set by the last score workgroup)
+  uint32_t pad0;
+  float scale[4];          // -lr * clip / max(||g_v||, clip) per variable
+  float loss;
+  float pad1[7];
+};
 
 // Everything a step kernel needs, passed by value (kernarg segment).
 struct StepArgs {
@@ -38,18 +53,18 @@ struct StepArgs {
   int32_t nP;       // positives per score workgroup = kStepWaves / wpp
   int32_t SW;       // negative slots per wave
   int32_t nWG;      // score workgroups
-  int32_t Kp;       // per-positive stride of the LDS score arrays (>= Keff + 1)
-  int32_t slotmax;  // keys per score workgroup = nP * (Keff + 3)
-  int32_t P;        // destination buckets (= entity/relation workgroups of the update kernel)
-  int64_t bs;       // destinations per bucket; destinations = [0, E) entities, [E, E+R) relations
+  int32_t cap;      // destination list capacity (entries per destination)
   int32_t snap_cols, gcols, rel_gcols;
+  uint32_t nkeyneg; // B * Keff: codes below are negatives (i * Keff + j), above positive rows
   // workspace
+  StepCtl* ctl;
   float2* coef;     // [B*Keff] (alpha, reduced value) per negative
   float* snap;      // [B, NSNAP, snap_cols] positive contexts
   float* gpos;      // [B, 3, gcols] positive h / r / t row gradients
   float* part;      // [nWG, 8] loss, norm^2 x4 partials
-  uint64_t* sorted; // [nWG, slotmax] keys dest << 32 | code, grouped by bucket
-  uint32_t* bmap;   // [P, nWG] start << 16 | count of bucket b in workgroup w
+  uint32_t* cnt;    // [E + R] entries per destination (zero between steps)
+  uint32_t* list;   // [E + R, cap] codes per destination (arrival order)
+  uint64_t* ovf;    // [B * (Keff + 3)] dest << 32 | code past a full list
   // KGE_OPT_GRAD outputs: dense [E, ent.cols] / [R, rel_gcols]
   float* gent;
   float* grel;
@@ -65,7 +80,7 @@ struct StepArgs {
 struct StepGeom {
   int vec, nc;
   int nWG, gridU;
-  size_t lds_score, lds_update;
+  size_t lds_score;
 };
 
 kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int model, int sk,
@@ -74,32 +89,26 @@ kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int mod
 __global__ void constrain_rows_kernel(float* t, int64_t rows, int32_t cols, int64_t ld, int kind,
                                       float value);
 
-}  // namespace kge
-
-namespace kge {
-
 // Byte offsets of the score kernel's dynamic LDS carve (shared by host and
 // device so the launch size always matches the kernel's view).
 struct ScoreLds {
-  int red, sR, sti, ssc, sM, ids, bkt, misc, sw, pos, cnt, total;
+  int pos, ids, sR, sT, st, mrg, red, posg, misc, total;
 };
 
 __host__ __device__ inline int lds_align16(int x) { return (x + 15) & ~15; }
 
-__host__ __device__ inline ScoreLds score_lds(int FL, int nP, int Kp, int Keff, int slotmax, int P) {
+__host__ __device__ inline ScoreLds score_lds(int FL, int nP, int Keff) {
   ScoreLds L;
   int o = 0;
-  L.red = o;  o += lds_align16(kStepWaves * 3 * FL * 4);
-  L.sR = o;   o += lds_align16(nP * Kp * 4);
-  L.sti = o;  o += lds_align16(nP * Kp * 4);
-  L.ssc = o;  o += lds_align16(nP * Kp * 4);
-  L.sM = o;   o += lds_align16(nP * Kp * 4);
-  L.ids = o;  o += lds_align16(nP * Keff * 4);
-  L.bkt = o;  o += lds_align16(slotmax * 4);
-  L.misc = o; o += lds_align16(kStepWaves * 8 * 4);
-  L.sw = o;   o += lds_align16(16 * 4);
   L.pos = o;  o += lds_align16(nP * 3 * 8);
-  L.cnt = o;  o += lds_align16((P + 1) * 4);
+  L.ids = o;  o += lds_align16(nP * Keff * 4);
+  L.sR = o;   o += lds_align16(nP * Keff * 4);
+  L.sT = o;   o += lds_align16(nP * Keff * 4);
+  L.st = o;   o += lds_align16(kStepWaves * 8 * 4);
+  L.mrg = o;  o += lds_align16(nP * kMergeStride * 4);
+  L.red = o;  o += lds_align16(kStepWaves * 3 * FL * 4);
+  L.posg = o; o += lds_align16(nP * 3 * FL * 4);
+  L.misc = o; o += lds_align16(kStepWaves * 8 * 4);
   L.total = o;
   return L;
 }

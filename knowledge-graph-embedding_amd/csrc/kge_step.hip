@@ -6,33 +6,33 @@
 //   K0  constrain   full-table row renormalisation of ent_emb when the model's
 //                   _constraint_loss assigns it (TransE.py:171-172,
 //                   DistMult.py:162-163).
-//   KS  score       8-wave workgroups; `wpp` waves per positive. In-register
+//   KS  score       8-wave workgroups, `wpp` waves per positive. In-register
 //                   Philox negative draws (ns_strategy.py:39-64 in the layout
-//                   of BaseModel.py:332-408); each wave issues the gathers of
-//                   ALL its sampled rows at once (up to 32 rows in flight per
-//                   wave, kept in registers through the loss epilogue, so no
-//                   row is read twice); batched wave64 shuffle reductions for
-//                   the scores (score.py); the loss epilogue per positive in
-//                   LDS (loss.py; SANS softmax); analytic gradients: the
-//                   positive's own rows are reduced on chip, every negative
-//                   leaves one scalar coefficient. Finally the workgroup's
-//                   destination keys (entities AND the positive's relation)
-//                   are grouped by destination bucket (stable LDS counting
-//                   sort) for the update kernel.
-//   KU  update      destination-major, one workgroup per bucket: merges every
-//                   score workgroup's keys for its rows (LDS bitonic sort,
-//                   parallel segment scan), re-derives each negative's row
-//                   gradient from ONE frozen context row + its coefficient
-//                   (4 entries' loads in flight per wave), sums in registers,
-//                   applies clip_by_norm(5) per variable (BaseModel.py:327,
-//                   TF-2.5 IndexedSlices: norm over un-deduplicated slices)
-//                   and the SGD update (BaseModel.py:328, keras SGD
-//                   ResourceScatterAdd) with ONE read-modify-write per touched
-//                   row. No float atomics; fixed summation order, so results
-//                   are bit-reproducible.
+//                   of BaseModel.py:332-408); each wave streams its slots'
+//                   rows in register batches (gather -> forward -> ONE
+//                   transposed multi-reduction per batch -> loss weight ->
+//                   backward), with SANS's softmax folded in online (loss.py
+//                   :174-182), so every sampled row is read exactly once. The
+//                   positive's own rows are reduced on chip; every negative
+//                   leaves one (alpha, value) coefficient and its destination
+//                   key, filed straight into that destination's list (one
+//                   int atomic per key). The last workgroup reduces the
+//                   loss and the per-variable gradient norms (clip_by_norm,
+//                   BaseModel.py:327) in a fixed order.
+//   KU  update      destination-major, one wave per entity / relation row:
+//                   its keys in ascending code order (bit-reproducible sums,
+//                   no float atomics), each negative's row gradient re-derived
+//                   from ONE frozen context row + its coefficient, the
+//                   positives' own row gradients added, clip scale and SGD
+//                   (BaseModel.py:328, keras SGD ResourceScatterAdd) applied
+//                   with ONE read-modify-write per touched row.
 #include "kge_step.h"
 
 namespace kge {
+
+#ifdef KGE_PHASE_PROF
+__device__ unsigned long long g_kge_prof[64];
+#endif
 
 // ------------------------------------------------------------ K0 constrain
 // kind 0: normalized_embeddings(p=2) -> X / pow(sum X^2, 1/2) * value
@@ -121,44 +121,92 @@ __device__ __forceinline__ int slot_kind(int side_mode, int j) {
   return side_mode == KGE_SIDE_H ? KIND_HC : KIND_TC;
 }
 
-template <int N>
-__device__ __forceinline__ void wave_sum_n(float (&x)[N]) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-#pragma unroll
-    for (int u = 0; u < N; ++u) x[u] += __shfl_xor(x[u], o, KGE_WAVE);
-  }
+// ------------------------------------------------------------ cross-lane
+// Lane pairings used by the reductions. Bits 5 and 4 go through the gfx950
+// half-exchange instructions (v_permlane32_swap / v_permlane16_swap); bits
+// 3..0 through DPP: row_mirror (l ^ 15), row_half_mirror (l ^ 7),
+// quad_perm [2,3,0,1] (l ^ 2), quad_perm [1,0,3,2] (l ^ 1). Each pairing
+// flips lane bit B, and together they span all 64 lanes.
+template <int B> struct PairCtl;
+template <> struct PairCtl<3> { static constexpr int v = 0x140; };
+template <> struct PairCtl<2> { static constexpr int v = 0x141; };
+template <> struct PairCtl<1> { static constexpr int v = 0x4E; };
+template <> struct PairCtl<0> { static constexpr int v = 0xB1; };
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
-template <int N>
-__device__ __forceinline__ void wave_max_n(float (&x)[N]) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-#pragma unroll
-    for (int u = 0; u < N; ++u) x[u] = fmaxf(x[u], __shfl_xor(x[u], o, KGE_WAVE));
+template <bool MAX>
+__device__ __forceinline__ float comb(float a, float b) { return MAX ? fmaxf(a, b) : a + b; }
+
+// half exchange across lane bit B (5 or 4): lo = a with the high side's a
+// moved in, hi = b with the low side's b moved in (v_permlane{32,16}_swap)
+template <int B>
+__device__ __forceinline__ void half_swap(float a, float b, float& lo, float& hi) {
+  const unsigned ua = __builtin_bit_cast(unsigned, a), ub = __builtin_bit_cast(unsigned, b);
+  if constexpr (B == 5) {
+    const auto r = __builtin_amdgcn_permlane32_swap(ua, ub, false, false);
+    lo = __builtin_bit_cast(float, (unsigned)r[0]);
+    hi = __builtin_bit_cast(float, (unsigned)r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(ua, ub, false, false);
+    lo = __builtin_bit_cast(float, (unsigned)r[0]);
+    hi = __builtin_bit_cast(float, (unsigned)r[1]);
   }
 }
 
-// exclusive scan of one int per thread over the whole (kStepThreads) block
-__device__ __forceinline__ int block_scan_excl(int v, int* s_w, int* total) {
-  const int lane = lane_id(), wv = wave_id();
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < KGE_WAVE; o <<= 1) {
-    const int y = __shfl_up(x, o, KGE_WAVE);
-    if (lane >= o) x += y;
+// all-lane reduction of one value over lane bits [0, B]
+template <int B, bool MAX>
+__device__ __forceinline__ float lane_reduce(float v) {
+  if constexpr (B < 0) {
+    return v;
+  } else {
+    if constexpr (B >= 4) {
+      float x, y;
+      half_swap<B>(v, v, x, y);
+      v = comb<MAX>(x, y);
+    } else {
+      v = comb<MAX>(v, dpp_mov<PairCtl<B>::v>(v));
+    }
+    return lane_reduce<B - 1, MAX>(v);
   }
-  if (lane == KGE_WAVE - 1) s_w[wv] = x;
-  __syncthreads();
-  int off = 0, tot = 0;
+}
+
+// Transposed multi-reduction: N per-lane partials (N a power of two <= 64)
+// -> lane l holds the wave-wide reduction of value (l >> (6 - log2 N)).
+// Each step halves the list: a lane keeps one half, sends the other to its
+// partner and adds what it receives, so N values cost N - 1 + (6 - log2 N)
+// exchanges instead of 6 N.
+template <int N, bool MAX, int B = 5>
+__device__ __forceinline__ float multi_reduce(const float (&x)[N]) {
+  if constexpr (N == 1) {
+    return lane_reduce<B, MAX>(x[0]);
+  } else {
+    constexpr int H = N / 2;
+    float y[H];
+    if constexpr (B >= 4) {
 #pragma unroll
-  for (int k = 0; k < kStepWaves; ++k) {
-    const int t = s_w[k];
-    off += k < wv ? t : 0;
-    tot += t;
+      for (int k = 0; k < H; ++k) {
+        float lo, hi;
+        half_swap<B>(x[k], x[H + k], lo, hi);
+        y[k] = comb<MAX>(lo, hi);
+      }
+    } else {
+      const bool up = (lane_id() >> B) & 1;
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        const float keep = up ? x[H + k] : x[k];
+        const float send = up ? x[k] : x[H + k];
+        y[k] = comb<MAX>(keep, dpp_mov<PairCtl<B>::v>(send));
+      }
+    }
+    return multi_reduce<H, MAX, B - 1>(y);
   }
-  __syncthreads();
-  *total = tot;
-  return off + x - v;
+}
+
+__device__ __forceinline__ float bcast(float v, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
 
 // relation-row fragments: full layout, or RotatE's half layout
@@ -188,35 +236,75 @@ __device__ __forceinline__ void store_rel_row(const float (&v)[(HALF ? (VEC / 2 
   }
 }
 
+// dL/ds of one negative (loss.py); SANS with its positive's final softmax
+// reference max Ms and 1/Z
+__device__ __forceinline__ float neg_coef(const StepArgs& A, float s, float sp, float Ms, float invZ) {
+  switch (A.loss_kind) {
+    case KGE_LOSS_HINGE: return (A.margin + s - sp >= 0.f) ? A.inv_bk : 0.f;
+    case KGE_LOSS_LOGISTIC: { const float ex = expf(s - sp); return ex / (1.f + ex); }
+    case KGE_LOSS_BCE: return sigmoid(s) * A.inv_b;
+    case KGE_LOSS_SANS: return expf(A.temperature * s - Ms) * invZ * sigmoid(s + A.margin) * A.inv_b;
+    default: return s * A.inv_b;
+  }
+}
+
+// one destination key: append its code to the destination's list (arrival
+// order), or to the overflow list once that list is full
+__device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_t code) {
+  const uint32_t r = atomicAdd(&A.cnt[dest], 1u);
+  if (r < (uint32_t)A.cap) {
+    A.list[dest * A.cap + r] = code;
+  } else {
+    const uint32_t o = atomicAdd(&A.ctl->ovf_count, 1u);
+    A.ovf[o] = ((uint64_t)dest << 32) | code;
+  }
+}
+
+// per-positive merge slots (LDS)
+enum { MG_F = 0, MG_AP = 8, MG_LOSS = 9, MG_N = 10, MG_UN = 16, MG_RP = 20, MG_TP = 21, MG_SP = 22, MG_LPP = 23,
+       MG_RSQ = 24, MG_MS = 25, MG_IZ = 26, MG_STRIDE = kMergeStride };
+static_assert(MG_IZ < MG_STRIDE, "merge slots exceed the LDS stride");
+
 // ------------------------------------------------------------ KS score
+// One workgroup = kStepWaves waves = nP positives x wpp waves. A wave owns
+// SW consecutive negative slots of its positive and streams them in batches
+// of ROWS rows held in registers: gather (one global_load_dwordx4 per row
+// per lane), forward, ONE transposed multi-reduction for the whole batch,
+// per-row loss weight computed by the lanes that hold that row's score,
+// analytic backward into the positive's h / r / t accumulators. SANS's
+// softmax is folded in online (running max; accumulators rescaled when it
+// grows), so no row outlives its batch and no row is read twice. The
+// positive's waves merge their states through LDS; then every wave
+// finalises its slots' coefficients and files every destination key into
+// that destination's list for the update kernel.
 template <template <int, int, int> class Model, int VEC, int NC, int SK>
-__global__ __launch_bounds__(kStepThreads) void score_kernel(StepArgs A) {
+__global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4))) void score_kernel(StepArgs A) {
   using M = Model<VEC, NC, SK>;
   using F = Frag<VEC, NC>;
   constexpr int W = kStepWaves;
   constexpr int FL = KGE_WAVE * VEC * NC;   // floats per fragment image
-  constexpr int ROWS = 32 / NC;             // sampled rows resident per wave
+  constexpr int ROWS = 8 / NC > 1 ? 8 / NC : 2;   // rows per batch (in registers)
+  constexpr int SH = ROWS == 16 ? 2 : ROWS == 8 ? 3 : ROWS == 4 ? 4 : 5;   // lane l holds row l >> SH after multi_reduce
+  constexpr int LPR = 1 << SH;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
-  const int Keff = A.Keff, nP = A.nP, wpp = A.wpp, Kp = A.Kp;
-  const ScoreLds L = score_lds(FL, nP, Kp, Keff, A.slotmax, A.P);
-  float* red = reinterpret_cast<float*>(smem + L.red);      // [W][3][FL]
-  float* s_R = reinterpret_cast<float*>(smem + L.sR);       // [nP][Kp] reduced value
-  float* s_ti = reinterpret_cast<float*>(smem + L.sti);     // [nP][Kp] p=inf ties
-  float* s_sc = reinterpret_cast<float*>(smem + L.ssc);     // [nP][Kp] score -> alpha
-  float* s_M = reinterpret_cast<float*>(smem + L.sM);       // [nP][Kp] lp -> reduced value
-  int32_t* s_ids = reinterpret_cast<int32_t*>(smem + L.ids);
-  int32_t* s_bkt = reinterpret_cast<int32_t*>(smem + L.bkt);
-  float* s_misc = reinterpret_cast<float*>(smem + L.misc);
-  int32_t* s_w = reinterpret_cast<int32_t*>(smem + L.sw);
+  const int Keff = A.Keff, nP = A.nP, wpp = A.wpp;
+  const ScoreLds L = score_lds(FL, nP, Keff);
   int64_t* s_pos = reinterpret_cast<int64_t*>(smem + L.pos);
-  int32_t* s_cnt = reinterpret_cast<int32_t*>(smem + L.cnt);
+  int32_t* s_ids = reinterpret_cast<int32_t*>(smem + L.ids);
+  float* s_R = reinterpret_cast<float*>(smem + L.sR);
+  float* s_T = reinterpret_cast<float*>(smem + L.sT);
+  float* s_st = reinterpret_cast<float*>(smem + L.st);
+  float* s_mrg = reinterpret_cast<float*>(smem + L.mrg);
+  float* red = reinterpret_cast<float*>(smem + L.red);
+  float* posg = reinterpret_cast<float*>(smem + L.posg);
+  float* s_misc = reinterpret_cast<float*>(smem + L.misc);
+  __shared__ int s_last;
 
+  KGE_PROF_INIT();
   const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
   const int grp = wv / wpp, gw = wv % wpp;
   const MP mp{A.limit};
-  float nrm[4] = {0.f, 0.f, 0.f, 0.f};
-  float loss_acc = 0.f;
   int err = 0;
 
   const int64_t i0 = (int64_t)blockIdx.x * nP;
@@ -252,228 +340,256 @@ __global__ __launch_bounds__(kStepThreads) void score_kernel(StepArgs A) {
     s_ids[s] = (int32_t)e;
   }
   __syncthreads();
+  KGE_PROF(0);
 
   const bool active = grp < nValid;
   const int64_t i = i0 + grp;
+  const int jbeg = min(Keff, gw * A.SW);
+  const int jend = min(Keff, jbeg + A.SW);
+  const int32_t* ids = s_ids + grp * Keff;
+  float* gR = s_R + grp * Keff;
+  float* gT = s_T + grp * Keff;
+
   typename M::Ctx ctx;
+  float Mrun = -INFINITY, Zs = 0.f, lsum = 0.f, csum = 0.f;
+  float nrm[4] = {0.f, 0.f, 0.f, 0.f};
+  F accH, accR, accT;
+  accH.zero(); accR.zero(); accT.zero();
+  float Rp = 0.f, tp = 1.f, sp = 0.f, lpp = 0.f;
   if (active) {
     M::load_ctx(ctx, A.ent, A.rel, s_pos[grp * 3 + 0], s_pos[grp * 3 + 1], s_pos[grp * 3 + 2], mp);
-  }
-  const int jbeg = gw * A.SW;
-  const int jend = min(Keff, jbeg + A.SW);
-  const int nchunk = (A.SW + ROWS - 1) / ROWS;
-  const int32_t* ids = s_ids + grp * Keff;
-  float* gR = s_R + grp * Kp;
-  float* gT = s_ti + grp * Kp;
-  float* gS = s_sc + grp * Kp;
-  float* gM = s_M + grp * Kp;
-
-  F E[ROWS];
-  // ---- phase A: scores (slot Keff = the positive, done by the group's last wave)
-  if (active) {
-    if (gw == wpp - 1) {
+    {   // the positive's score, in every wave (hinge / logistic weights need it)
       F a, b, E0;
       E0.zero();
       M::fwd(ctx, KIND_POS, E0, a, b);
       const float part = score_partial<SK, M::CPLX>(a, b);
-      const float Rv = SK == SK_PINF ? wave_max(part) : wave_sum(part);
-      float ti = 1.f;
-      if (SK == SK_PINF) ti = wave_sum(tie_partial<M::CPLX>(a, Rv));
-      if (lane == 0) { gR[Keff] = Rv; gT[Keff] = ti; }
+      Rp = lane_reduce<5, SK == SK_PINF>(part);
+      if (SK == SK_PINF) tp = lane_reduce<5, false>(tie_partial<M::CPLX>(a, Rp));
+      sp = score_value<SK>(Rp, A.pw, &lpp);
     }
-    for (int c = 0; c < nchunk; ++c) {
-      const int j0 = jbeg + c * ROWS;
+    const int lrow = lane >> SH;
+    const bool lead = (lane & (LPR - 1)) == 0;
+    int idv = 0;   // the wave's next 64 slot ids, one per lane
+    for (int j0 = jbeg; j0 < jend; j0 += ROWS) {
+      if (((j0 - jbeg) & (KGE_WAVE - 1)) == 0) idv = (j0 + lane < jend) ? ids[j0 + lane] : 0;
+      const int jo = (j0 - jbeg) & (KGE_WAVE - 1);
+      F E[ROWS];
 #pragma unroll
-      for (int u = 0; u < ROWS; ++u)
-        if (j0 + u < jend) load_row(E[u], A.ent.row(ids[j0 + u]), A.ent.cols);
+      for (int u = 0; u < ROWS; ++u) {
+        // wave-uniform row id (readlane -> SGPR): scalar base address per row
+        if (j0 + u < jend) load_row(E[u], A.ent.row(__builtin_amdgcn_readlane(idv, jo + u)), A.ent.cols);
+        else E[u].zero();
+      }
       float part[ROWS];
 #pragma unroll
       for (int u = 0; u < ROWS; ++u) {
-        part[u] = 0.f;
-        if (j0 + u < jend) {
-          F a, b;
-          M::fwd(ctx, slot_kind(A.side_mode, j0 + u), E[u], a, b);
-          part[u] = score_partial<SK, M::CPLX>(a, b);
-        }
+        F a, b;
+        M::fwd(ctx, slot_kind(A.side_mode, j0 + u), E[u], a, b);
+        part[u] = (j0 + u < jend) ? score_partial<SK, M::CPLX>(a, b) : 0.f;
       }
-      if (SK == SK_PINF) {
-        wave_max_n(part);
-        float tp[ROWS];
+      const float Rl = multi_reduce<ROWS, SK == SK_PINF>(part);
+      float tl = 1.f;
+      if constexpr (SK == SK_PINF) {
+        float tq[ROWS];
 #pragma unroll
         for (int u = 0; u < ROWS; ++u) {
-          tp[u] = 0.f;
-          if (j0 + u < jend) {
-            F a, b;
-            M::fwd(ctx, slot_kind(A.side_mode, j0 + u), E[u], a, b);
-            tp[u] = tie_partial<M::CPLX>(a, part[u]);
-          }
+          const float Ru = bcast(Rl, u << SH);
+          F a, b;
+          M::fwd(ctx, slot_kind(A.side_mode, j0 + u), E[u], a, b);
+          tq[u] = (j0 + u < jend) ? tie_partial<M::CPLX>(a, Ru) : 0.f;
         }
-        wave_sum_n(tp);
-        if (lane == 0) {
-#pragma unroll
-          for (int u = 0; u < ROWS; ++u)
-            if (j0 + u < jend) { gR[j0 + u] = part[u]; gT[j0 + u] = tp[u]; }
-        }
-      } else {
-        wave_sum_n(part);
-        if (lane == 0) {
-#pragma unroll
-          for (int u = 0; u < ROWS; ++u)
-            if (j0 + u < jend) { gR[j0 + u] = part[u]; gT[j0 + u] = 1.f; }
-        }
+        tl = multi_reduce<ROWS, false>(tq);
       }
-    }
-  }
-  __syncthreads();
-
-  // ---- loss epilogue (first wave of each group): c_j = dL/ds_j -> alpha_j
-  if (active && gw == 0) {
-    float lpp;
-    const float sp = score_value<SK>(gR[Keff], A.pw, &lpp);
-    float zmax = -INFINITY;
-    for (int j = lane; j < Keff; j += KGE_WAVE) {
-      float lpj;
-      const float sj = score_value<SK>(gR[j], A.pw, &lpj);
-      gS[j] = sj;
-      gM[j] = lpj;   // keep lp for alpha
-      zmax = fmaxf(zmax, A.temperature * sj);
-    }
-    zmax = wave_max(zmax);
-    float Z = 0.f;
-    if (A.loss_kind == KGE_LOSS_SANS)
-      for (int j = lane; j < Keff; j += KGE_WAVE) Z += expf(A.temperature * gS[j] - zmax);
-    Z = wave_sum(Z);
-    float lsum = 0.f, csum = 0.f;
-    for (int j = lane; j < Keff; j += KGE_WAVE) {
-      const float sj = gS[j];
+      const int j = j0 + lrow;
+      const bool valid = j < jend;
+      float lp;
+      const float s = score_value<SK>(Rl, A.pw, &lp);
       float c = 0.f;
       switch (A.loss_kind) {
         case KGE_LOSS_HINGE: {
-          const float m = A.margin + sj - sp;
-          lsum += fmaxf(m, 0.f);
+          const float m = A.margin + s - sp;
           c = (m >= 0.f) ? A.inv_bk : 0.f;
+          if (valid && lead) { lsum += fmaxf(m, 0.f); csum += c; }
         } break;
         case KGE_LOSS_LOGISTIC: {
-          const float ex = expf(sj - sp);
-          lsum += logf(1.f + ex);
+          const float ex = expf(s - sp);
           c = ex / (1.f + ex);
+          if (valid && lead) { lsum += logf(1.f + ex); csum += c; }
         } break;
         case KGE_LOSS_BCE:
-          lsum += log_sigmoid(-sj);
-          c = sigmoid(sj) * A.inv_b;
+          c = sigmoid(s) * A.inv_b;
+          if (valid && lead) lsum += log_sigmoid(-s);
           break;
         case KGE_LOSS_SANS: {
-          const float pj = expf(A.temperature * sj - zmax) / Z;
-          lsum += pj * log_sigmoid(-sj - A.margin);
-          c = pj * sigmoid(sj + A.margin) * A.inv_b;
+          const float z = valid ? A.temperature * s : -INFINITY;
+          const float Mn = fmaxf(Mrun, lane_reduce<5, true>(z));
+          if (Mn > Mrun) {   // wave-uniform: rescale everything accumulated so far
+            const float sc = (Mrun == -INFINITY) ? 0.f : expf(Mrun - Mn);
+            const float sc2 = sc * sc;
+#pragma unroll
+            for (int q = 0; q < VEC * NC; ++q) { accH.v[q] *= sc; accR.v[q] *= sc; accT.v[q] *= sc; }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) nrm[v] *= sc2;
+            Zs *= sc;
+            lsum *= sc;
+            Mrun = Mn;
+          }
+          const float e = valid ? expf(z - Mrun) : 0.f;
+          c = e * sigmoid(s + A.margin) * A.inv_b;
+          if (valid && lead) { Zs += e; lsum += e * log_sigmoid(-s - A.margin); }
         } break;
         default:  // SQERR
-          lsum += sj * sj;
-          c = sj * A.inv_b;
+          c = s * A.inv_b;
+          if (valid && lead) lsum += s * s;
           break;
       }
-      csum += c;
-      const float al = score_alpha<SK>(c, gR[j], gM[j], gT[j], A.pw);
-      const float Mj = gR[j];
-      if (A.train) A.coef[i * Keff + j] = make_float2(al, Mj);
-      gM[j] = Mj;
-      gS[j] = al;   // alpha (scores already consumed)
-      if (A.neg_score_out) A.neg_score_out[i * Keff + j] = sj;
+      const float al = valid ? score_alpha<SK>(c, Rl, lp, tl, A.pw) : 0.f;
+      if (valid && lead) { gR[j] = Rl; gT[j] = tl; }
+#pragma unroll
+      for (int u = 0; u < ROWS; ++u) {
+        if (j0 + u < jend) {
+          const float alu = bcast(al, u << SH);
+          const float Mu = SK == SK_PINF ? bcast(Rl, u << SH) : 0.f;
+          const int kind = slot_kind(A.side_mode, j0 + u);
+          F a, b;
+          M::fwd(ctx, kind, E[u], a, b);
+          M::bwd(ctx, kind, E[u], a, b, alu, Mu, accH, accR, accT, nrm, mp);
+        }
+      }
     }
-    lsum = wave_sum(lsum);
-    csum = wave_sum(csum);
-    // DistMult constraint term lambda * mean_i ||r_i||^2 (DistMult.py:164-165)
-    float rreg = 0.f;
-    if (A.rel_reg != 0.f) {
+  }
+  KGE_PROF(1);
+
+  // ---- wave state -> LDS
+  {
+    const float Zw = wave_sum(Zs), lw = wave_sum(lsum), cw = wave_sum(csum);
+    float nw[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) nw[v] = wave_sum(nrm[v]);
+    if (lane == 0) {
+      float* st = s_st + wv * 8;
+      st[0] = Mrun; st[1] = Zw; st[2] = lw; st[3] = cw;
+      st[4] = nw[0]; st[5] = nw[1]; st[6] = nw[2]; st[7] = nw[3];
+    }
+    if (A.train) {
+      float* my = red + wv * 3 * FL;
+#pragma unroll
+      for (int q = 0; q < VEC * NC; ++q) {
+        const int c = q / VEC, k = q % VEC;
+        const int e = (c * KGE_WAVE + lane) * VEC + k;
+        my[e] = accH.v[q];
+        my[FL + e] = accR.v[q];
+        my[2 * FL + e] = accT.v[q];
+      }
+    }
+  }
+  // the positive's own gradient at unit alpha (wave 0 of each positive)
+  if (active && gw == 0) {
+    float* mg = s_mrg + grp * MG_STRIDE;
+    float pn[4] = {0.f, 0.f, 0.f, 0.f};
+    if (A.train) {
+      F pH, pR, pT, a, b, E0;
+      pH.zero(); pR.zero(); pT.zero(); E0.zero();
+      M::fwd(ctx, KIND_POS, E0, a, b);
+      M::bwd(ctx, KIND_POS, E0, a, b, 1.f, Rp, pH, pR, pT, pn, mp);
+      float* pg = posg + grp * 3 * FL;
+#pragma unroll
+      for (int q = 0; q < VEC * NC; ++q) {
+        const int c = q / VEC, k = q % VEC;
+        const int e = (c * KGE_WAVE + lane) * VEC + k;
+        pg[e] = pH.v[q];
+        pg[FL + e] = pR.v[q];
+        pg[2 * FL + e] = pT.v[q];
+      }
+      M::write_snap(ctx, A.snap + i * (M::NSNAP * (int64_t)A.snap_cols), A.snap_cols);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) pn[v] = wave_sum(pn[v]);
+    float rsq = 0.f;
+    if (A.rel_reg != 0.f) {   // DistMult: lambda * mean_i ||r_i||^2 (DistMult.py:164-165)
       F Rr;
       load_row(Rr, A.rel.row(s_pos[grp * 3 + 1]), A.rel.cols);
-      rreg = wave_sum(sq_partial(Rr)) * A.rel_reg * A.inv_b;
+      rsq = wave_sum(sq_partial(Rr));
     }
     if (lane == 0) {
-      loss_acc += rreg;
-      float cp, lossp;
-      switch (A.loss_kind) {
-        case KGE_LOSS_HINGE:
-          lossp = lsum * A.inv_bk;
-          cp = -csum;
-          if (Keff == 0) lossp = NAN;   // sum([]) / 0 (loss.py:81-82)
-          break;
-        case KGE_LOSS_LOGISTIC: lossp = lsum; cp = -csum; break;
-        case KGE_LOSS_BCE:
-          lossp = -(log_sigmoid(sp) + lsum) * A.inv_b;
-          cp = -sigmoid(-sp) * A.inv_b;
-          break;
-        case KGE_LOSS_SANS:
-          lossp = -(log_sigmoid(sp + A.margin) + lsum) * A.inv_b;
-          cp = -sigmoid(-(sp + A.margin)) * A.inv_b;
-          break;
-        default:
-          lossp = ((sp - 1.f) * (sp - 1.f) + lsum) * 0.5f * A.inv_b;
-          cp = (sp - 1.f) * A.inv_b;
-          break;
-      }
-      loss_acc += lossp;
-      gS[Keff] = score_alpha<SK>(cp, gR[Keff], lpp, gT[Keff], A.pw);
-      gM[Keff] = gR[Keff];
-      if (A.pos_score_out) A.pos_score_out[i] = sp;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) mg[MG_UN + v] = pn[v];
+      mg[MG_RP] = Rp; mg[MG_TP] = tp; mg[MG_SP] = sp; mg[MG_LPP] = lpp; mg[MG_RSQ] = rsq;
     }
   }
   __syncthreads();
+  KGE_PROF(2);
 
+  // ---- merge the positive's waves (one thread per positive)
+  if (tid < nValid) {
+    const int p = tid;
+    float* mg = s_mrg + p * MG_STRIDE;
+    const float* st = s_st + p * wpp * 8;
+    const bool sans = A.loss_kind == KGE_LOSS_SANS;
+    float Ms = -INFINITY;
+    for (int g = 0; g < wpp; ++g) Ms = fmaxf(Ms, st[g * 8]);
+    float f[kMaxWpp];
+    float Z = 0.f, lw = 0.f, cw = 0.f;
+    for (int g = 0; g < wpp; ++g) {
+      const float sc = !sans ? 1.f : (st[g * 8] == -INFINITY ? 0.f : expf(st[g * 8] - Ms));
+      f[g] = sc;
+      Z += st[g * 8 + 1] * sc;
+      lw += st[g * 8 + 2] * sc;
+      cw += st[g * 8 + 3];
+    }
+    const float invZ = sans ? (Z > 0.f ? 1.f / Z : 0.f) : 1.f;
+    lw *= invZ;
+    const float Rpv = mg[MG_RP], tpv = mg[MG_TP], spv = mg[MG_SP], lppv = mg[MG_LPP];
+    float lossp, cp;
+    switch (A.loss_kind) {
+      case KGE_LOSS_HINGE:
+        lossp = lw * A.inv_bk;
+        cp = -cw;
+        if (Keff == 0) lossp = NAN;   // sum([]) / 0 (loss.py:81-82)
+        break;
+      case KGE_LOSS_LOGISTIC: lossp = lw; cp = -cw; break;
+      case KGE_LOSS_BCE:
+        lossp = -(log_sigmoid(spv) + lw) * A.inv_b;
+        cp = -sigmoid(-spv) * A.inv_b;
+        break;
+      case KGE_LOSS_SANS:
+        lossp = -(log_sigmoid(spv + A.margin) + lw) * A.inv_b;
+        cp = -sigmoid(-(spv + A.margin)) * A.inv_b;
+        break;
+      default:
+        lossp = ((spv - 1.f) * (spv - 1.f) + lw) * 0.5f * A.inv_b;
+        cp = (spv - 1.f) * A.inv_b;
+        break;
+    }
+    const float ap = score_alpha<SK>(cp, Rpv, lppv, tpv, A.pw);
+    float n[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) n[v] = ap * ap * mg[MG_UN + v];
+    for (int g = 0; g < wpp; ++g) {
+      const float fg = f[g] * invZ;
+      mg[MG_F + g] = fg;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) n[v] += fg * fg * st[g * 8 + 4 + v];
+    }
+    if (A.rel_reg != 0.f) {
+      // its own IndexedSlices block: (lambda / B) * 2 r  (pow-2 gradient)
+      const float gsc = A.rel_reg * A.inv_b;
+      lossp += mg[MG_RSQ] * gsc;
+      n[1] += 4.f * gsc * gsc * mg[MG_RSQ];
+    }
+    mg[MG_AP] = ap;
+    mg[MG_LOSS] = lossp;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) mg[MG_N + v] = n[v];
+    mg[MG_MS] = Ms;
+    mg[MG_IZ] = invZ;
+    if (A.pos_score_out) A.pos_score_out[i0 + p] = spv;
+  }
+  __syncthreads();
+  KGE_PROF(3);
+
+  // ---- the positives' row gradients: sum of the waves' scaled accumulators
   if (A.train) {
-    // ---- phase B: analytic gradients (rows still resident when nchunk == 1)
-    F accH, accR, accT;
-    accH.zero(); accR.zero(); accT.zero();
-    if (active) {
-      if (gw == wpp - 1) {
-        F a, b, E0;
-        E0.zero();
-        M::fwd(ctx, KIND_POS, E0, a, b);
-        M::bwd(ctx, KIND_POS, E0, a, b, gS[Keff], gM[Keff], accH, accR, accT, nrm, mp);
-      }
-      if (A.rel_reg != 0.f && gw == 0) {
-        // its own IndexedSlices block: (lambda / B) * 2 r  (pow-2 gradient)
-        F Rr;
-        load_row(Rr, A.rel.row(s_pos[grp * 3 + 1]), A.rel.cols);
-        const float gsc = A.rel_reg * A.inv_b;
-#pragma unroll
-        for (int q = 0; q < VEC * NC; ++q) {
-          const float g = gsc * (2.f * Rr.v[q]);
-          accR.v[q] += g;
-          nrm[1] += g * g;
-        }
-      }
-      for (int c = 0; c < nchunk; ++c) {
-        const int j0 = jbeg + c * ROWS;
-        if (nchunk > 1) {
-#pragma unroll
-          for (int u = 0; u < ROWS; ++u)
-            if (j0 + u < jend) load_row(E[u], A.ent.row(ids[j0 + u]), A.ent.cols);
-        }
-#pragma unroll
-        for (int u = 0; u < ROWS; ++u) {
-          const int j = j0 + u;
-          if (j < jend) {
-            const int kind = slot_kind(A.side_mode, j);
-            F a, b;
-            M::fwd(ctx, kind, E[u], a, b);
-            M::bwd(ctx, kind, E[u], a, b, gS[j], gM[j], accH, accR, accT, nrm, mp);
-          }
-        }
-      }
-    }
-    // cross-wave reduction of the positive's row gradients
-    float* my = red + wv * 3 * FL;
-#pragma unroll
-    for (int q = 0; q < VEC * NC; ++q) {
-      const int c = q / VEC, k = q % VEC;
-      const int e = (c * KGE_WAVE + lane) * VEC + k;
-      my[e] = accH.v[q];
-      my[FL + e] = accR.v[q];
-      my[2 * FL + e] = accT.v[q];
-    }
-    if (active && gw == 0) M::write_snap(ctx, A.snap + i * (M::NSNAP * (int64_t)A.snap_cols), A.snap_cols);
-    __syncthreads();
     for (int e = tid; e < nValid * 3 * FL; e += blockDim.x) {
       const int p = e / (3 * FL), rem = e % (3 * FL);
       const int v = rem / FL, k = rem % FL;
@@ -481,360 +597,287 @@ __global__ __launch_bounds__(kStepThreads) void score_kernel(StepArgs A) {
       if (k >= cols) continue;
       // RotatE keeps the phase gradient of complex element k in float 2k
       const int src = (v == 1 && A.rel_half) ? 2 * k : k;
-      float s = 0.f;
-      for (int g = 0; g < wpp; ++g) s += red[((p * wpp + g) * 3 + v) * FL + src];
+      const float* mg = s_mrg + p * MG_STRIDE;
+      float s = mg[MG_AP] * posg[(p * 3 + v) * FL + src];
+      for (int g = 0; g < wpp; ++g) s += mg[MG_F + g] * red[((p * wpp + g) * 3 + v) * FL + src];
+      if (v == 1 && A.rel_reg != 0.f) s += (A.rel_reg * A.inv_b) * (2.f * A.rel.row(s_pos[p * 3 + 1])[k]);
       A.gpos[(i0 + p) * 3 * (int64_t)A.gcols + v * (int64_t)A.gcols + k] = s;
     }
   }
 
-  // ---- per-workgroup partials: loss, norm^2 per variable (fixed order)
-#pragma unroll
-  for (int v = 0; v < 4; ++v) nrm[v] = wave_sum(nrm[v]);
-  if (lane == 0) {
-    s_misc[wv * 8] = loss_acc;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) s_misc[wv * 8 + 1 + v] = nrm[v];
-  }
-  if (err) set_status(A.status, err);
-  __syncthreads();
-  if (tid < 5) {
-    float s = 0.f;
-    for (int w = 0; w < W; ++w) s += s_misc[w * 8 + tid];
-    A.part[(int64_t)blockIdx.x * 8 + tid] = s;
-  }
-  if (!A.train) return;
-
-  // ---- group the workgroup's destination keys by bucket (stable counting sort)
-  // key = dest << 32 | code; dest < E: entity, dest >= E: relation dest - E.
-  // code < nP*Keff: negative slot; else nP*Keff + 3p + {0: h, 1: t, 2: r}.
-  const int Kn = nP * Keff;
-  const int nNeg = nValid * Keff;
-  const int nKeys = nNeg + 3 * nValid;
-  const int64_t E_ = A.ent.rows;
-  auto key_of = [&](int s) -> uint64_t {
-    if (s < nNeg) return ((uint64_t)(uint32_t)s_ids[s] << 32) | (uint32_t)s;
-    const int q = s - nNeg, p = q / 3, c = q % 3;
-    const int64_t dest = c == 0 ? s_pos[p * 3] : c == 1 ? s_pos[p * 3 + 2] : E_ + s_pos[p * 3 + 1];
-    return ((uint64_t)dest << 32) | (uint32_t)(Kn + q);
-  };
-  for (int b = tid; b <= A.P; b += blockDim.x) s_cnt[b] = 0;
-  __syncthreads();
-  for (int s = tid; s < nKeys; s += blockDim.x) {
-    const int b = (int)((int64_t)(key_of(s) >> 32) / A.bs);
-    s_bkt[s] = b;
-    atomicAdd(&s_cnt[b], 1);
-  }
-  __syncthreads();
-  {
-    const int CP = (A.P + blockDim.x - 1) / blockDim.x;
-    const int b0 = tid * CP, b1 = min(A.P, b0 + CP);
-    int local = 0;
-    for (int b = b0; b < b1; ++b) local += s_cnt[b];
-    int total;
-    int run = block_scan_excl(local, s_w, &total);
-    for (int b = b0; b < b1; ++b) {
-      const int c = s_cnt[b];
-      A.bmap[(int64_t)b * A.nWG + blockIdx.x] = ((uint32_t)run << 16) | (uint32_t)c;
-      s_cnt[b] = run;
-      run += c;
+  // ---- each wave finalises its slots: coefficient, score, destination key
+  if (active && (A.train || A.neg_score_out)) {
+    const float* mg = s_mrg + grp * MG_STRIDE;
+    const float Ms = mg[MG_MS], invZ = mg[MG_IZ], spv = mg[MG_SP];
+    for (int j = jbeg + lane; j < jend; j += KGE_WAVE) {
+      const float R = gR[j];
+      float lp;
+      const float s = score_value<SK>(R, A.pw, &lp);
+      const int64_t q = i * Keff + j;
+      if (A.neg_score_out) A.neg_score_out[q] = s;
+      if (A.train) {
+        const float c = neg_coef(A, s, spv, Ms, invZ);
+        A.coef[q] = make_float2(score_alpha<SK>(c, R, lp, gT[j], A.pw), R);
+        bin_key(A, ids[j], (uint32_t)q);
+      }
     }
   }
-  __syncthreads();
-  uint64_t* out = A.sorted + (int64_t)blockIdx.x * A.slotmax;
-  for (int s = tid; s < nKeys; s += blockDim.x) {
-    const int b = s_bkt[s];
-    int rank = 0;
-    for (int s2 = 0; s2 < s; ++s2) rank += s_bkt[s2] == b;   // LDS broadcast reads
-    out[s_cnt[b] + rank] = key_of(s);
+  if (A.train && tid < nValid * 3) {
+    const int p = tid / 3, c = tid % 3;
+    const int64_t dest = c == 0 ? s_pos[p * 3] : c == 1 ? s_pos[p * 3 + 2] : A.ent.rows + s_pos[p * 3 + 1];
+    bin_key(A, dest, A.nkeyneg + (uint32_t)(3 * (i0 + p) + c));
   }
-}
+  if (err) set_status(A.status, err);
+  KGE_PROF(4);
 
-// ------------------------------------------------------------ KU update
-// blocks [0, P): destination buckets of bs consecutive destinations. Block 0
-// also reduces the loss. Dynamic LDS: s_list [kUCap] u64, s_segs [kUCap+4],
-// red [W][FL] (overflow path).
-template <template <int, int, int> class Model, int VEC, int NC, int SK>
-__global__ __launch_bounds__(kStepThreads) void update_kernel(StepArgs A) {
-  using M = Model<VEC, NC, SK>;
-  using F = Frag<VEC, NC>;
-  constexpr int W = kStepWaves;
-  constexpr int FL = KGE_WAVE * VEC * NC;
-  constexpr int U = NC == 1 ? 4 : NC == 2 ? 2 : 1;   // entries in flight per wave
-  constexpr int RV = RelV<M::CPLX, VEC>::n;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint64_t* s_list = reinterpret_cast<uint64_t*>(smem);
-  int32_t* s_segs = reinterpret_cast<int32_t*>(s_list + kUCap);
-  float* red = reinterpret_cast<float*>(s_segs + kUCap + 4);
-  __shared__ float s_part[W * 8];
-  __shared__ float s_scale[8];
-  __shared__ int s_w[16];
-  __shared__ int s_flag;
-
-  const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-
-  // ---- clip_by_norm scale per variable: clip / max(||g||, clip), and the loss
-  {
+  // ---- workgroup partials; the last workgroup to finish reduces them in a
+  // fixed order and publishes the clip scales and the loss
+  if (tid == 0) {
     float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int w = tid; w < A.nWG; w += blockDim.x) {
+    for (int p = 0; p < nValid; ++p) {
+      const float* mg = s_mrg + p * MG_STRIDE;
+      acc[0] += mg[MG_LOSS];
 #pragma unroll
-      for (int k = 0; k < 5; ++k) acc[k] += A.part[(int64_t)w * 8 + k];
+      for (int v = 0; v < 4; ++v) acc[1 + v] += mg[MG_N + v];
+    }
+    // publish: write-through (agent-scope) stores, drained before the ticket
+    // add -- no L2 write-back fence (MI355X: one per workgroup is costly)
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      __hip_atomic_store(&A.part[(int64_t)blockIdx.x * 8 + k], acc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);   // vmcnt / lgkmcnt / expcnt drained
+    const uint32_t prev = __hip_atomic_fetch_add(&A.ctl->score_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (uint32_t)(gridDim.x - 1);
+  }
+  __syncthreads();
+  if (s_last) {
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int w = tid; w < (int)gridDim.x; w += blockDim.x) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        acc[k] += __hip_atomic_load(&A.part[(int64_t)w * 8 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #pragma unroll
     for (int k = 0; k < 5; ++k) acc[k] = wave_sum(acc[k]);
     if (lane == 0) {
 #pragma unroll
-      for (int k = 0; k < 5; ++k) s_part[wv * 8 + k] = acc[k];
+      for (int k = 0; k < 5; ++k) s_misc[wv * 8 + k] = acc[k];
     }
     __syncthreads();
     if (tid < 5) {
       float s = 0.f;
-      for (int w = 0; w < W; ++w) s += s_part[w * 8 + tid];
+      for (int w = 0; w < W; ++w) s += s_misc[w * 8 + tid];
       if (tid == 0) {
-        if (blockIdx.x == 0) {
-          A.loss_out[0] = s;
-          if (A.loss_accum) A.loss_accum[0] += s;
-        }
+        A.loss_out[0] = s;
+        if (A.loss_accum) A.loss_accum[0] += s;
+        A.ctl->loss = s;
+        A.ctl->score_ticket = 0u;
+        // every workgroup's keys are filed: hand the overflow length to the
+        // update kernel and restart the overflow list for the next step
+        A.ctl->ovf_len = __hip_atomic_exchange(&A.ctl->ovf_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
-        s_scale[tid - 1] = -A.lr * (A.clip_norm / fmaxf(sqrtf(s), A.clip_norm));
-        if (blockIdx.x == 0 && A.norm2_out) A.norm2_out[tid - 1] = s;
+        A.ctl->scale[tid - 1] = -A.lr * (A.clip_norm / fmaxf(sqrtf(s), A.clip_norm));
+        if (A.norm2_out) A.norm2_out[tid - 1] = s;
       }
     }
-    __syncthreads();
   }
-  if (!A.train) return;
+  KGE_PROF(5);
+}
 
-  const int b = blockIdx.x;
-  const int64_t lo = (int64_t)b * A.bs;
+// ------------------------------------------------------------ KU update
+// Destination-major: one wave per destination row (entities [0, E), then
+// relations [E, E + R)). The wave reads its list of codes (filed in arrival
+// order by the score kernel) and visits them in ascending code order -- so
+// every row is summed in the same order on every run (bit-reproducible, no
+// float atomics). It re-derives each negative's row gradient from ONE
+// frozen context row + its coefficient, adds the positives' own row
+// gradients, and applies clip_by_norm(5) per variable (BaseModel.py:327;
+// TF-2.5 IndexedSlices: norm over un-deduplicated slices, reduced by the
+// score kernel) and the SGD update (BaseModel.py:328, keras SGD
+// ResourceScatterAdd) with ONE read-modify-write per touched row. The
+// destination's counter is cleared for the next step as it is read.
+template <template <int, int, int> class Model, int VEC, int NC, int SK>
+__global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
+  using M = Model<VEC, NC, SK>;
+  using F = Frag<VEC, NC>;
+  constexpr int U = NC == 1 ? 8 : NC == 2 ? 4 : 2;   // entries in flight per wave
+  constexpr int RV = RelV<M::CPLX, VEC>::n;
+  constexpr int CHMAX = 4;                            // in-register ordering up to 256 codes
+  __shared__ uint32_t s_scr[kUpdWaves][CHMAX * KGE_WAVE];
+
+  KGE_PROF_INIT();
+  const int lane = lane_id(), wv = wave_id();
   const int64_t E_ = A.ent.rows;
   const int64_t ndest = E_ + A.rel.rows;
-  const int Kn = A.nP * A.Keff;
+  const int64_t d = (int64_t)blockIdx.x * kUpdWaves + wv;
+  const uint32_t nneg = A.nkeyneg;
 
-  // ---- per-source-workgroup counts and a deterministic exclusive scan
-  const int CW = (A.nWG + blockDim.x - 1) / blockDim.x;
-  const int w0 = tid * CW, w1 = min(A.nWG, w0 + CW);
-  int local = 0;
-  for (int w = w0; w < w1; ++w) local += (int)(A.bmap[(int64_t)b * A.nWG + w] & 0xFFFFu);
-  int L;
-  const int base0 = block_scan_excl(local, s_w, &L);
-  if (L == 0) return;
-
-  // one key -> its positive's index i, and for a negative its slot j (c = -1);
-  // for a positive's own row c = 0 (h), 1 (t), 2 (r)
-  auto decode = [&](uint32_t lo32, int64_t* i, int* j, int* c) {
-    const int w = (int)(lo32 >> 16), code = (int)(lo32 & 0xFFFFu);
-    if (code < Kn) {
-      *i = (int64_t)w * A.nP + code / A.Keff;
-      *j = code % A.Keff;
+  // one code -> its positive i and slot j (negative, c = -1) or row part c (0 h, 1 t, 2 r)
+  auto decode = [&](uint32_t code, int64_t* i, int* j, int* c) {
+    if (code < nneg) {
+      const uint32_t q = code / (uint32_t)A.Keff;
+      *i = q;
+      *j = (int)(code - q * (uint32_t)A.Keff);
       *c = -1;
     } else {
-      const int q = code - Kn;
-      *i = (int64_t)w * A.nP + q / 3;
+      const uint32_t q = (code - nneg) / 3u;
+      *i = q;
       *j = 0;
-      *c = q % 3;
+      *c = (int)(code - nneg - q * 3u);
     }
   };
-  // entity destination: sum of the gradient rows of entries [s0, s1) of `src`
-  auto entity_sum = [&](const uint64_t* src, int s0, int s1, const F& E, F& acc) {
-    for (int s = s0; s < s1; s += U) {
-      int64_t ii[U];
-      int jj[U], cc[U];
-      typename M::ECtx ec[U];
-      float2 cf[U];
-      F gp[U];
+  // entity destination: add the gradient rows of `cntv` (<= U) entries
+  auto entity_add = [&](const uint32_t* codes, int cntv, const F& E, F& acc) {
+    int64_t ii[U];
+    int jj[U], cc[U];
+    typename M::ECtx ec[U];   // a positive's own row gradient goes into ec[u].c0
+    float2 cf[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (s + u < s1) {
-          decode((uint32_t)src[s + u], &ii[u], &jj[u], &cc[u]);
-          if (cc[u] < 0) {
-            cf[u] = A.coef[ii[u] * A.Keff + jj[u]];
-            M::load_ectx(A.snap + ii[u] * (M::NSNAP * (int64_t)A.snap_cols), A.snap_cols,
-                         slot_kind(A.side_mode, jj[u]), ec[u]);
-          } else {
-            load_row(gp[u], A.gpos + ii[u] * 3 * (int64_t)A.gcols + (cc[u] == 0 ? 0 : 2) * (int64_t)A.gcols,
-                     A.ent.cols);
-          }
+    for (int u = 0; u < U; ++u) {
+      if (u < cntv) {
+        decode(codes[u], &ii[u], &jj[u], &cc[u]);
+        if (cc[u] < 0) {
+          cf[u] = A.coef[ii[u] * A.Keff + jj[u]];
+          M::load_ectx(A.snap + ii[u] * (M::NSNAP * (int64_t)A.snap_cols), A.snap_cols,
+                       slot_kind(A.side_mode, jj[u]), ec[u]);
+        } else {
+          load_row(ec[u].c0, A.gpos + ii[u] * 3 * (int64_t)A.gcols + (cc[u] == 0 ? 0 : 2) * (int64_t)A.gcols,
+                   A.ent.cols);
         }
       }
+    }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (s + u < s1) {
-          if (cc[u] < 0) {
-            F g;
-            M::grad_entity(ec[u], slot_kind(A.side_mode, jj[u]), E, cf[u].x, cf[u].y, g);
-            add_to(acc, g);
-          } else {
-            add_to(acc, gp[u]);
-          }
+    for (int u = 0; u < U; ++u) {
+      if (u < cntv) {
+        if (cc[u] < 0) {
+          F g;
+          M::grad_entity(ec[u], slot_kind(A.side_mode, jj[u]), E, cf[u].x, cf[u].y, g);
+          add_to(acc, g);
+        } else {
+          add_to(acc, ec[u].c0);
         }
       }
     }
   };
-  auto rel_sum = [&](const uint64_t* src, int s0, int s1, float (&acc)[RV * NC]) {
-    for (int s = s0; s < s1; s += U) {
-      float g[U][RV * NC];
+  auto rel_add = [&](const uint32_t* codes, int cntv, float (&acc)[RV * NC]) {
+    float g[U][RV * NC];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (s + u < s1) {
-          int64_t ii;
-          int jj, cc;
-          decode((uint32_t)src[s + u], &ii, &jj, &cc);
-          load_rel_row<M::CPLX, VEC, NC>(g[u], A.gpos + ii * 3 * (int64_t)A.gcols + A.gcols, A.rel_gcols);
-        }
+    for (int u = 0; u < U; ++u) {
+      if (u < cntv) {
+        int64_t ii;
+        int jj, cc;
+        decode(codes[u], &ii, &jj, &cc);
+        load_rel_row<M::CPLX, VEC, NC>(g[u], A.gpos + ii * 3 * (int64_t)A.gcols + A.gcols, A.rel_gcols);
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (s + u < s1) {
-#pragma unroll
-          for (int q = 0; q < RV * NC; ++q) acc[q] += g[u][q];
-        }
     }
-  };
-  auto apply_entity = [&](int64_t e, F& E, const F& acc) {
-    if (A.grad_mode) {
-      store_row(acc, A.gent + e * (int64_t)A.ent.cols, A.ent.cols);
-      return;
-    }
-    const float sc = s_scale[0];
 #pragma unroll
-    for (int q = 0; q < VEC * NC; ++q) E.v[q] = E.v[q] + acc.v[q] * sc;
-    store_row(E, A.ent.row_w(e), A.ent.cols);
-  };
-  auto apply_rel = [&](int64_t r, const float (&acc)[RV * NC]) {
-    if (A.grad_mode) {
-      store_rel_row<M::CPLX, VEC, NC>(acc, A.grel + r * (int64_t)A.rel_gcols, A.rel.cols);
-      return;
-    }
-    float row[RV * NC];
-    load_rel_row<M::CPLX, VEC, NC>(row, A.rel.row(r), A.rel.cols);
-    const float sc = s_scale[1];
+    for (int u = 0; u < U; ++u)
+      if (u < cntv) {
 #pragma unroll
-    for (int q = 0; q < RV * NC; ++q) row[q] = row[q] + acc[q] * sc;
-    store_rel_row<M::CPLX, VEC, NC>(row, A.rel.row_w(r), A.rel.cols);
+        for (int q = 0; q < RV * NC; ++q) acc[q] += g[u][q];
+      }
   };
 
-  if (L <= kUCap) {
-    // ---- fast path: gather the bucket's keys into LDS, sort, segment.
-    // key' = (dest - lo) << 32 | w << 16 | code
-    int base = base0;
-    for (int w = w0; w < w1; ++w) {
-      const uint32_t pk = A.bmap[(int64_t)b * A.nWG + w];
-      const int st = (int)(pk >> 16), cnt = (int)(pk & 0xFFFFu);
-      const uint64_t* src = A.sorted + (int64_t)w * A.slotmax + st;
-      for (int k = 0; k < cnt; ++k) {
-        const uint64_t key = src[k];
-        s_list[base++] = (((key >> 32) - (uint64_t)lo) << 32) | ((uint64_t)w << 16) | (key & 0xFFFFu);
-      }
-    }
-    int Lp = 1;
-    while (Lp < L) Lp <<= 1;
-    for (int s = L + tid; s < Lp; s += blockDim.x) s_list[s] = ~0ull;
-    __syncthreads();
-    for (int k = 2; k <= Lp; k <<= 1) {
-      for (int jj = k >> 1; jj > 0; jj >>= 1) {
-        for (int s = tid; s < Lp; s += blockDim.x) {
-          const int o = s ^ jj;
-          if (o > s) {
-            const uint64_t x = s_list[s], y = s_list[o];
-            const bool up = (s & k) == 0;
-            if ((x > y) == up) { s_list[s] = y; s_list[o] = x; }
+  if (d < ndest) {
+    const uint32_t n = A.cnt[d];
+    if (n != 0u) {
+      if (lane == 0) A.cnt[d] = 0u;   // ready for the next step
+      const bool is_ent = d < E_;
+      F E, acc;
+      acc.zero();
+      E.zero();
+      float racc[RV * NC];
+#pragma unroll
+      for (int q = 0; q < RV * NC; ++q) racc[q] = 0.f;
+      if (is_ent) load_row(E, A.ent.row(d), A.ent.cols);
+      const uint32_t* lst = A.list + d * (int64_t)A.cap;
+      if (n <= (uint32_t)A.cap && n <= (uint32_t)(CHMAX * KGE_WAVE)) {
+        // ascending code order: each code's rank among the n (codes are unique)
+        const int nch = (int)((n + KGE_WAVE - 1) / KGE_WAVE);
+        uint32_t code[CHMAX];
+#pragma unroll
+        for (int c = 0; c < CHMAX; ++c) {
+          const uint32_t q = (uint32_t)(c * KGE_WAVE + lane);
+          code[c] = (c < nch && q < n) ? lst[q] : 0xFFFFFFFFu;
+        }
+        uint32_t rank[CHMAX] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int c2 = 0; c2 < CHMAX; ++c2) {
+          if (c2 < nch) {
+            const int lim = min(KGE_WAVE, (int)n - c2 * KGE_WAVE);
+            for (int q = 0; q < lim; ++q) {
+              const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)code[c2], q);
+#pragma unroll
+              for (int c = 0; c < CHMAX; ++c) rank[c] += (o < code[c]) ? 1u : 0u;
+            }
           }
         }
-        __syncthreads();
-      }
-    }
-    // segment starts (ordered): block scan of head flags
-    const int CL = (L + blockDim.x - 1) / blockDim.x;
-    const int l0 = tid * CL, l1 = min(L, l0 + CL);
-    int heads = 0;
-    for (int s = l0; s < l1; ++s)
-      heads += (s == 0 || (s_list[s] >> 32) != (s_list[s - 1] >> 32)) ? 1 : 0;
-    int nseg;
-    int sidx = block_scan_excl(heads, s_w, &nseg);
-    for (int s = l0; s < l1; ++s)
-      if (s == 0 || (s_list[s] >> 32) != (s_list[s - 1] >> 32)) s_segs[sidx++] = s;
-    if (tid == 0) s_segs[nseg] = L;
-    __syncthreads();
-    for (int sg = wv; sg < nseg; sg += W) {
-      const int s0 = s_segs[sg], s1 = s_segs[sg + 1];
-      const int64_t dest = lo + (int64_t)(s_list[s0] >> 32);
-      if (dest < E_) {
-        F E, acc;
-        load_row(E, A.ent.row(dest), A.ent.cols);
-        acc.zero();
-        entity_sum(s_list, s0, s1, E, acc);
-        apply_entity(dest, E, acc);
+        uint32_t* scr = s_scr[wv];
+#pragma unroll
+        for (int c = 0; c < CHMAX; ++c)
+          if (c < nch && (uint32_t)(c * KGE_WAVE + lane) < n) scr[rank[c]] = code[c];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int p0 = 0; p0 < (int)n; p0 += U) {
+          uint32_t cs[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) cs[u] = (uint32_t)__builtin_amdgcn_readfirstlane((int)scr[min(p0 + u, (int)n - 1)]);
+          if (is_ent) entity_add(cs, min(U, (int)n - p0), E, acc);
+          else rel_add(cs, min(U, (int)n - p0), racc);
+        }
       } else {
-        float acc[RV * NC];
+        // a list past its capacity: repeated selection of the next code from
+        // the list and the overflow entries (correct for any skew, not fast)
+        const uint32_t nl = min(n, (uint32_t)A.cap);
+        const uint32_t novf = A.ctl->ovf_len;
+        uint32_t last = 0u;
+        for (uint32_t p = 0; p < n; ++p) {
+          uint32_t best = 0xFFFFFFFFu;
+          for (uint32_t q = lane; q < nl; q += KGE_WAVE) {
+            const uint32_t x = lst[q];
+            if ((p == 0u || x > last) && x < best) best = x;
+          }
+          for (uint32_t q = lane; q < novf; q += KGE_WAVE) {
+            const uint64_t y = A.ovf[q];
+            const uint32_t x = (uint32_t)y;
+            if ((int64_t)(y >> 32) == d && (p == 0u || x > last) && x < best) best = x;
+          }
 #pragma unroll
-        for (int q = 0; q < RV * NC; ++q) acc[q] = 0.f;
-        rel_sum(s_list, s0, s1, acc);
-        apply_rel(dest - E_, acc);
+          for (int o = 32; o >= 1; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, KGE_WAVE));
+          last = best;
+          uint32_t cs[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) cs[u] = best;
+          if (is_ent) entity_add(cs, 1, E, acc);
+          else rel_add(cs, 1, racc);
+        }
       }
-    }
-    return;
-  }
-
-  // ---- overflow path: destination by destination; waves split the source
-  // workgroups (w = wv mod W), partial sums combined in wave order.
-  const int64_t d_hi = min<int64_t>(ndest, lo + A.bs);
-  for (int64_t dest = lo; dest < d_hi; ++dest) {
-    const bool is_ent = dest < E_;
-    F E, acc;
-    acc.zero();
-    E.zero();
-    if (is_ent) load_row(E, A.ent.row(dest), A.ent.cols);
-    float racc[RV * NC];
-#pragma unroll
-    for (int q = 0; q < RV * NC; ++q) racc[q] = 0.f;
-    bool any = false;
-    for (int w = wv; w < A.nWG; w += W) {
-      const uint32_t pk = A.bmap[(int64_t)b * A.nWG + w];
-      const int st = (int)(pk >> 16), cnt = (int)(pk & 0xFFFFu);
-      const uint64_t* src = A.sorted + (int64_t)w * A.slotmax + st;
-      for (int k = 0; k < cnt; ++k) {
-        const uint64_t key = src[k];
-        if ((int64_t)(key >> 32) != dest) continue;
-        const uint64_t k2 = ((uint64_t)w << 16) | (key & 0xFFFFu);
-        if (is_ent) entity_sum(&k2, 0, 1, E, acc);
-        else rel_sum(&k2, 0, 1, racc);
-        any = true;
-      }
-    }
-    if (tid == 0) s_flag = 0;
-    __syncthreads();
-    if (any && lane == 0) atomicOr(&s_flag, 1);
-#pragma unroll
-    for (int q = 0; q < VEC * NC; ++q) {
-      const int c = q / VEC, k = q % VEC;
-      const int idx = (c * KGE_WAVE + lane) * VEC + k;
-      red[wv * FL + idx] = is_ent ? acc.v[q] : (q < RV * NC ? racc[q] : 0.f);
-    }
-    __syncthreads();
-    if (wv == 0 && s_flag) {
       if (is_ent) {
+        if (A.grad_mode) {
+          store_row(acc, A.gent + d * (int64_t)A.ent.cols, A.ent.cols);
+        } else {
+          const float sc = A.ctl->scale[0];
 #pragma unroll
-        for (int q = 0; q < VEC * NC; ++q) {
-          const int c = q / VEC, k = q % VEC;
-          const int idx = (c * KGE_WAVE + lane) * VEC + k;
-          float s = 0.f;
-          for (int w = 0; w < W; ++w) s += red[w * FL + idx];
-          acc.v[q] = s;
+          for (int q = 0; q < VEC * NC; ++q) E.v[q] = E.v[q] + acc.v[q] * sc;
+          store_row(E, A.ent.row_w(d), A.ent.cols);
         }
-        apply_entity(dest, E, acc);
       } else {
+        const int64_t r = d - E_;
+        if (A.grad_mode) {
+          store_rel_row<M::CPLX, VEC, NC>(racc, A.grel + r * (int64_t)A.rel_gcols, A.rel.cols);
+        } else {
+          float row[RV * NC];
+          load_rel_row<M::CPLX, VEC, NC>(row, A.rel.row(r), A.rel.cols);
+          const float sc = A.ctl->scale[1];
 #pragma unroll
-        for (int q = 0; q < RV * NC; ++q) {
-          const int c = q / VEC, k = q % VEC;
-          const int idx = (c * KGE_WAVE + lane) * VEC + k;
-          float s = 0.f;
-          for (int w = 0; w < W; ++w) s += red[w * FL + idx];
-          racc[q] = s;
+          for (int q = 0; q < RV * NC; ++q) row[q] = row[q] + racc[q] * sc;
+          store_rel_row<M::CPLX, VEC, NC>(row, A.rel.row_w(r), A.rel.cols);
         }
-        apply_rel(dest - E_, racc);
       }
     }
-    __syncthreads();
   }
+  KGE_PROF(16);
 }
 
 // ------------------------------------------------------------ dispatch
@@ -842,11 +885,13 @@ template <template <int, int, int> class Model, int VEC, int NC, int SK>
 static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_t st, hipEvent_t const* ev) {
   hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK>), dim3(G.nWG), dim3(kStepThreads), G.lds_score, st, A);
   if (ev) (void)hipEventRecord(ev[2], st);
-  hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK>), dim3(A.train ? G.gridU : 1), dim3(kStepThreads),
-                     G.lds_update, st, A);
+  if (A.train)
+    hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
   return KGE_OK;
 }
 
+
+#ifndef KGE_ONLY_ONE
 template <template <int, int, int> class Model, int VEC, int NC>
 static kge_status by_sk(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st, hipEvent_t const* ev) {
   switch (sk) {
@@ -903,14 +948,33 @@ static kge_status rotate(const StepArgs& A, const StepGeom& G, int sk, hipStream
   return by_sk_lp<RotatE, 2, 4>(A, G, sk, st, ev);
 }
 
+#endif  // KGE_ONLY_ONE
+
 kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int model, int sk,
                                    hipStream_t st, hipEvent_t const* ev) {
+#ifdef KGE_ONLY_ONE
+  // quick-iteration builds (tools/phase_prof.py): the bench's C2 instance only
+  if (model == KGE_MODEL_TRANSE && G.vec == 4 && G.nc == 1 && sk == SK_P2)
+    return launch_family<TransE, 4, 1, SK_P2>(A, G, st, ev);
+  return KGE_EUNSUPPORTED;
+#else
   switch (model) {
     case KGE_MODEL_TRANSE: return transe(A, G, sk, st, ev);
     case KGE_MODEL_DISTMULT: return distmult(A, G, st, ev);
     case KGE_MODEL_ROTATE: return rotate(A, G, sk, st, ev);
     default: return KGE_EUNSUPPORTED;
   }
+#endif
 }
 
 }  // namespace kge
+
+#ifdef KGE_PHASE_PROF
+// profiling builds: read / reset the per-phase tick counters
+extern "C" int kge_prof_read(unsigned long long* out, int n) {
+  if (n > 64) n = 64;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(kge::g_kge_prof), n * sizeof(unsigned long long)) != hipSuccess) return 1;
+  unsigned long long z[64] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(kge::g_kge_prof), z, sizeof(z)) != hipSuccess;
+}
+#endif

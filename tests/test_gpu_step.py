@@ -71,7 +71,7 @@ def _spec_loss(lf):
 
 
 def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, idx=torch.int64, train=True,
-             seed=11, constraint=True, typed=None, lr=0.05, opt="sgd"):
+             seed=11, constraint=True, typed=None, lr=0.05, opt="sgd", flags=0):
     from KGE import engine, optimizers
     from KGE.ns_strategy import TypedStrategy, UniformStrategy
     dev = _dev()
@@ -85,6 +85,7 @@ def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, id
     m = _make(model_name, d, K, side, score_fn, loss_fn, E, R, sampler, constraint)
     m.model_weights = {k: torch.tensor(v, device=dev) for k, v in W.items()}
     step = engine.FusedStep(m)
+    step.flags = flags
     Keff = 2 * (K // 2) if side == "h+t" else K
     ps = torch.zeros(B, dtype=torch.float32, device=dev)
     ns = torch.zeros(B * Keff, dtype=torch.float32, device=dev)
@@ -191,6 +192,46 @@ def test_tiny_entity_set_overflow_path(hiplib):
     ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransE", 16, 300, 40, "h+t", score.LpDistance(2),
                                           loss.SelfAdversarialNegativeSamplingLoss(1.0, 0.5), E=3, R=2)
     check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("li", [0, 3])
+def test_destination_list_overflow(hiplib, li):
+    """KGE_FLAG_DEBUG_LIST_CAP: 4-entry destination lists, so most keys go
+    through the overflow list and the update kernel's selection path."""
+    from KGE import score
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransE", 32, 24, 16, "h+t", score.LpDistance(2),
+                                          _losses()[li], E=40, R=5, flags=2)
+    check(ref, got, l_, ps, ns)
+
+
+def test_consecutive_steps_reuse_workspace(hiplib):
+    """Three steps through one FusedStep (one workspace: tickets, list counters
+    and the overflow counter must reset themselves) == three oracle steps."""
+    from KGE import engine, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    dev = _dev()
+    rng = np.random.default_rng(21)
+    E, R, d, B, K = 60, 6, 48, 33, 10
+    W = _weights("TransE", E, R, d, rng)
+    sampler = UniformStrategy(np.arange(E), seed=4)
+    m = _make("TransE", d, K, "h+t", score.LpDistance(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
+              E, R, sampler)
+    m.model_weights = {k: torch.tensor(v, device=dev) for k, v in W.items()}
+    step = engine.FusedStep(m)
+    opt = optimizers.SGD(0.05)
+    ref_w = W
+    for it in range(3):
+        pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+        plane = sampler.offset
+        step(torch.tensor(pos, device=dev), True, opt)
+        torch.cuda.synchronize()
+        step.check_status()
+        neg = orc.negatives(pos, K, "h+t", E, seed=4, plane=plane)
+        ref = orc.train_step("TransE", ref_w, pos, neg, score=("lp", 2.0), loss=("sans", 3.0, 1.0), lr=0.05)
+        ref_w = ref["weights"]
+        assert abs(float(step.loss_out.item()) - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"])), it
+        for k, v in ref_w.items():
+            np.testing.assert_allclose(m.model_weights[k].cpu().numpy(), v, atol=TOL, err_msg="%s step %d" % (k, it))
 
 
 def test_hinge_zero_negatives_is_nan(hiplib):
