@@ -143,7 +143,9 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   int wpp = 1;
   while (wpp < kMaxWpp && (int64_t)wpp * 64 < Keff) wpp <<= 1;
   const int nP = kStepWaves / wpp;
-  const int SW = std::max<int>(1, (int)ceil_div(Keff, wpp));
+  // 'h+t': even slot ranges, so every stream batch starts on an h-corrupt slot
+  int SW = std::max<int>(1, (int)ceil_div(Keff, wpp));
+  if (d->corrupt_side == KGE_SIDE_HT) SW = (int)round_up(SW, 2);
   const int64_t nWG = std::max<int64_t>(1, ceil_div(B, nP));
   if (nWG > 0x7fffffff) return fail(KGE_EUNSUPPORTED, "batch %lld too large", (long long)B);
   // destination keys: codes i*Keff + j (negatives), B*Keff + 3i + c (positive rows)

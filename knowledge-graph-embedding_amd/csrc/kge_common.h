@@ -161,6 +161,26 @@ __device__ __forceinline__ void load_row(Frag<VEC, NC>& f, const float* __restri
   }
 }
 
+// Unmasked: lanes past the row's end load its first element group and keep
+// it (callers mask what they reduce). cols >= VEC.
+template <int VEC, int NC>
+__device__ __forceinline__ void load_row_raw(Frag<VEC, NC>& f, const float* __restrict__ row, int cols) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int e0 = (c * KGE_WAVE + lane_id()) * VEC;
+    const int e = e0 < cols ? e0 : 0;
+    if (VEC == 4) {
+      const float4 x = *reinterpret_cast<const float4*>(row + e);
+      f.v[c * 4 + 0] = x.x; f.v[c * 4 + 1] = x.y; f.v[c * 4 + 2] = x.z; f.v[c * 4 + 3] = x.w;
+    } else if (VEC == 2) {
+      const float2 x = *reinterpret_cast<const float2*>(row + e);
+      f.v[c * 2 + 0] = x.x; f.v[c * 2 + 1] = x.y;
+    } else {
+      f.v[c] = row[e];
+    }
+  }
+}
+
 template <int VEC, int NC>
 __device__ __forceinline__ void store_row(const Frag<VEC, NC>& f, float* __restrict__ row, int cols) {
 #pragma unroll

@@ -102,6 +102,30 @@ __device__ __forceinline__ float score_alpha(float c, float R, float lp, float t
   return -clp / ties;
 }
 
+// Hardware-rate forms (v_sqrt / v_rsq, ~1 ulp) of score_value / score_alpha
+// for the score kernel's in-stream weights; the stored per-negative
+// coefficients and scores use the IEEE forms above.
+template <int SK>
+__device__ __forceinline__ float score_value_fast(float R, bool pw, float* lp_out) {
+  if (SK == SK_DOT) { *lp_out = R; return R; }
+  float lp;
+  if (SK == SK_P2) lp = -__builtin_amdgcn_sqrtf(fmaxf(R, 1e-9f));
+  else if (SK == SK_P1) lp = -fmaxf(R, 1e-9f);
+  else lp = -R;
+  *lp_out = lp;
+  return pw ? -(lp * lp) : lp;
+}
+template <int SK>
+__device__ __forceinline__ float score_alpha_fast(float c, float R, float lp, float ties, bool pw) {
+  if (SK == SK_DOT) return c;
+  const float clp = pw ? c * (-2.f * lp) : c;
+  if (SK == SK_P2) return R >= 1e-9f ? -clp * __builtin_amdgcn_rsqf(R) : 0.f;
+  if (SK == SK_P1) return R >= 1e-9f ? -clp : 0.f;
+  return -clp * __builtin_amdgcn_rcpf(ties);
+}
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+__device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + fast_exp(-x)); }
+
 // Element gradient wrt a (Lp kinds). M = max |a| (PINF only).
 template <int SK, bool CPLX, int VEC, int NC>
 __device__ __forceinline__ void score_grad(const Frag<VEC, NC>& a, float alpha, float M,
@@ -232,6 +256,53 @@ struct TransE {
     if (kind != KIND_HC) add_to(accH, gx);
     if (kind != KIND_TC) add_to(accT, gy);
   }
+  // ---- score-kernel stream hooks (slot kind known at compile time)
+  // Lp kinds: the t-slot gradient is minus the h-slot one, so a negative row
+  // adds to ONE accumulator (t-corrupted -> h, h-corrupted -> t) and the
+  // relation gradient is rebuilt once after the stream (finish): accR =
+  // accH - accT. P2: the row gradient is alpha * a, so its norm^2 is
+  // alpha^2 * R, accumulated from the reduced value (NRM_FROM_R).
+  static constexpr bool NRM_FROM_R = SK == SK_P2;
+  template <int KIND>
+  __device__ static void fwdk(const Ctx& c, const F& E, F& a, F& b) {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) {
+      if (SK == SK_DOT) {
+        a.v[i] = KIND == KIND_HC ? E.v[i] + c.R.v[i] : c.X.v[i];
+        b.v[i] = KIND == KIND_TC ? E.v[i] : c.T.v[i];
+      } else {
+        a.v[i] = KIND == KIND_HC ? E.v[i] + c.D.v[i] : c.X.v[i] - (KIND == KIND_TC ? E.v[i] : c.T.v[i]);
+      }
+    }
+  }
+  template <int KIND>
+  __device__ static void bwdk(const Ctx& c, const F& E, const F& a, const F& b, float alpha, float M,
+                              F& accH, F& accR, F& accT, float* nrm, const MP& mp) {
+    if (SK == SK_DOT) {
+      bwd(c, KIND, E, a, b, alpha, M, accH, accR, accT, nrm, mp);
+      return;
+    }
+    if (SK == SK_P2) {
+#pragma unroll
+      for (int i = 0; i < VEC * NC; ++i) {
+        if (KIND == KIND_TC) accH.v[i] += alpha * a.v[i];
+        else accT.v[i] -= alpha * a.v[i];
+      }
+      return;
+    }
+    F g;
+    score_grad<SK, false>(a, alpha, M, g);
+    const float s = sq_partial(g);
+    nrm[0] += 2.f * s;
+    nrm[1] += s;
+    if (KIND == KIND_TC) add_to(accH, g);
+    else sub_to(accT, g);
+  }
+  __device__ static void finish(F& accH, F& accR, F& accT) {
+    if (SK == SK_DOT) return;
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) accR.v[i] = accH.v[i] - accT.v[i];
+  }
   __device__ static void write_snap(const Ctx& c, float* sb, int cols) {
     store_row(c.X, sb, cols);
     if (SK == SK_DOT) {   // Dot: h-corrupted needs r and t separately -> keep r + t? use D slot for t
@@ -312,6 +383,16 @@ struct DistMult {
     if (kind != KIND_HC) add_to(accH, gH);
     if (kind != KIND_TC) add_to(accT, gT);
   }
+  // score-kernel stream hooks: slot kind known at compile time
+  static constexpr bool NRM_FROM_R = false;   // row-gradient norm^2 from the reduced value
+  template <int KIND>
+  __device__ static void fwdk(const Ctx& c, const F& E, F& a, F& b) { fwd(c, KIND, E, a, b); }
+  template <int KIND>
+  __device__ static void bwdk(const Ctx& c, const F& E, const F& a, const F& b, float alpha, float M,
+                              F& accH, F& accR, F& accT, float* nrm, const MP& mp) {
+    bwd(c, KIND, E, a, b, alpha, M, accH, accR, accT, nrm, mp);
+  }
+  __device__ static void finish(F& accH, F& accR, F& accT) {}
   __device__ static void write_snap(const Ctx& c, float* sb, int cols) {
     store_row(c.HR, sb, cols);
     store_row(c.TR, sb + cols, cols);
@@ -398,6 +479,16 @@ struct RotatE {
     if (kind != KIND_HC) add_to(accH, gH);
     if (kind != KIND_TC) sub_to(accT, gx);
   }
+  // score-kernel stream hooks: slot kind known at compile time
+  static constexpr bool NRM_FROM_R = false;   // row-gradient norm^2 from the reduced value
+  template <int KIND>
+  __device__ static void fwdk(const Ctx& c, const F& E, F& a, F& b) { fwd(c, KIND, E, a, b); }
+  template <int KIND>
+  __device__ static void bwdk(const Ctx& c, const F& E, const F& a, const F& b, float alpha, float M,
+                              F& accH, F& accR, F& accT, float* nrm, const MP& mp) {
+    bwd(c, KIND, E, a, b, alpha, M, accH, accR, accT, nrm, mp);
+  }
+  __device__ static void finish(F& accH, F& accR, F& accT) {}
   __device__ static void write_snap(const Ctx& c, float* sb, int cols) {
     store_row(c.X, sb, cols);
     store_row(c.CS, sb + cols, cols);

@@ -26,7 +26,13 @@
 //                   positives' own row gradients added, clip scale and SGD
 //                   (BaseModel.py:328, keras SGD ResourceScatterAdd) applied
 //                   with ONE read-modify-write per touched row.
+#include <utility>
+
 #include "kge_step.h"
+
+#ifndef KGE_STREAM_ROWS
+#define KGE_STREAM_ROWS 8   // sampled rows per stream batch at NC = 1 (tuning knob)
+#endif
 
 namespace kge {
 
@@ -260,6 +266,23 @@ __device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_
   }
 }
 
+// compile-time loop over u = 0 .. N-1 (fn gets std::integral_constant<int, u>)
+template <class Fn, int... Is>
+__device__ __forceinline__ void static_for_impl(Fn& fn, std::integer_sequence<int, Is...>) {
+  (fn(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class Fn>
+__device__ __forceinline__ void static_for(Fn&& fn) {
+  static_for_impl(fn, std::make_integer_sequence<int, N>{});
+}
+
+// corruption kind of row u of a stream batch (batches start on an even slot:
+// 'h+t' slots alternate h-corrupt / t-corrupt, BaseModel.py:353-356)
+template <int SIDE>
+__host__ __device__ constexpr int kind_at(int u) {
+  return SIDE == KGE_SIDE_HT ? ((u & 1) ? KIND_TC : KIND_HC) : SIDE == KGE_SIDE_H ? KIND_HC : KIND_TC;
+}
+
 // per-positive merge slots (LDS)
 enum { MG_F = 0, MG_AP = 8, MG_LOSS = 9, MG_N = 10, MG_UN = 16, MG_RP = 20, MG_TP = 21, MG_SP = 22, MG_LPP = 23,
        MG_RSQ = 24, MG_MS = 25, MG_IZ = 26, MG_STRIDE = kMergeStride };
@@ -277,13 +300,13 @@ static_assert(MG_IZ < MG_STRIDE, "merge slots exceed the LDS stride");
 // positive's waves merge their states through LDS; then every wave
 // finalises its slots' coefficients and files every destination key into
 // that destination's list for the update kernel.
-template <template <int, int, int> class Model, int VEC, int NC, int SK>
+template <template <int, int, int> class Model, int VEC, int NC, int SK, int SIDE>
 __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4))) void score_kernel(StepArgs A) {
   using M = Model<VEC, NC, SK>;
   using F = Frag<VEC, NC>;
   constexpr int W = kStepWaves;
   constexpr int FL = KGE_WAVE * VEC * NC;   // floats per fragment image
-  constexpr int ROWS = 8 / NC > 1 ? 8 / NC : 2;   // rows per batch (in registers)
+  constexpr int ROWS = KGE_STREAM_ROWS / NC > 1 ? KGE_STREAM_ROWS / NC : 2;   // rows per batch (in registers)
   constexpr int SH = ROWS == 16 ? 2 : ROWS == 8 ? 3 : ROWS == 4 ? 4 : 5;   // lane l holds row l >> SH after multi_reduce
   constexpr int LPR = 1 << SH;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -351,7 +374,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
   float* gT = s_T + grp * Keff;
 
   typename M::Ctx ctx;
-  float Mrun = -INFINITY, Zs = 0.f, lsum = 0.f, csum = 0.f;
+  float Mrun = -INFINITY, Zs = 0.f, csum = 0.f;
   float nrm[4] = {0.f, 0.f, 0.f, 0.f};
   F accH, accR, accT;
   accH.zero(); accR.zero(); accT.zero();
@@ -369,106 +392,114 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
     }
     const int lrow = lane >> SH;
     const bool lead = (lane & (LPR - 1)) == 0;
+    // RAW: unmasked row loads, only the score partial masked (NRM_FROM_R
+    // models keep no per-element norm, single-chunk rows)
+    constexpr bool RAW = M::NRM_FROM_R && NC == 1;
+    const bool lane_in = lane * VEC < A.ent.cols;
     int idv = 0;   // the wave's next 64 slot ids, one per lane
     for (int j0 = jbeg; j0 < jend; j0 += ROWS) {
       if (((j0 - jbeg) & (KGE_WAVE - 1)) == 0) idv = (j0 + lane < jend) ? ids[j0 + lane] : 0;
       const int jo = (j0 - jbeg) & (KGE_WAVE - 1);
+      const int nrow = min(ROWS, jend - j0);   // wave-uniform, >= 1
+      // every row's load is issued before any is used; rows past the slot
+      // range repeat the last valid row (finite values, weight 0)
+      // (NRM_FROM_R models: lanes past the row's end keep whatever they
+      // loaded and only their score partial is masked -- their accumulator
+      // lanes are never read back)
       F E[ROWS];
 #pragma unroll
       for (int u = 0; u < ROWS; ++u) {
-        // wave-uniform row id (readlane -> SGPR): scalar base address per row
-        if (j0 + u < jend) load_row(E[u], A.ent.row(__builtin_amdgcn_readlane(idv, jo + u)), A.ent.cols);
-        else E[u].zero();
+        const float* row = A.ent.row(__builtin_amdgcn_readlane(idv, jo + min(u, nrow - 1)));
+        if (RAW) load_row_raw(E[u], row, A.ent.cols);
+        else load_row(E[u], row, A.ent.cols);
       }
+      F a[ROWS], b[ROWS];
       float part[ROWS];
-#pragma unroll
-      for (int u = 0; u < ROWS; ++u) {
-        F a, b;
-        M::fwd(ctx, slot_kind(A.side_mode, j0 + u), E[u], a, b);
-        part[u] = (j0 + u < jend) ? score_partial<SK, M::CPLX>(a, b) : 0.f;
-      }
+      static_for<ROWS>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        M::template fwdk<kind_at<SIDE>(u)>(ctx, E[u], a[u], b[u]);
+        part[u] = (u < nrow && (!RAW || lane_in)) ? score_partial<SK, M::CPLX>(a[u], b[u]) : 0.f;
+      });
       const float Rl = multi_reduce<ROWS, SK == SK_PINF>(part);
       float tl = 1.f;
       if constexpr (SK == SK_PINF) {
         float tq[ROWS];
 #pragma unroll
-        for (int u = 0; u < ROWS; ++u) {
-          const float Ru = bcast(Rl, u << SH);
-          F a, b;
-          M::fwd(ctx, slot_kind(A.side_mode, j0 + u), E[u], a, b);
-          tq[u] = (j0 + u < jend) ? tie_partial<M::CPLX>(a, Ru) : 0.f;
-        }
+        for (int u = 0; u < ROWS; ++u) tq[u] = u < nrow ? tie_partial<M::CPLX>(a[u], bcast(Rl, u << SH)) : 0.f;
         tl = multi_reduce<ROWS, false>(tq);
       }
       const int j = j0 + lrow;
-      const bool valid = j < jend;
+      const bool valid = lrow < nrow;
+      // this lane's row weight dL/ds (loss.py; the loss VALUE is summed in
+      // the finalise pass), hardware-rate transcendentals
       float lp;
-      const float s = score_value<SK>(Rl, A.pw, &lp);
+      const float s = score_value_fast<SK>(Rl, A.pw, &lp);
       float c = 0.f;
       switch (A.loss_kind) {
-        case KGE_LOSS_HINGE: {
-          const float m = A.margin + s - sp;
-          c = (m >= 0.f) ? A.inv_bk : 0.f;
-          if (valid && lead) { lsum += fmaxf(m, 0.f); csum += c; }
-        } break;
+        case KGE_LOSS_HINGE:
+          c = (A.margin + s - sp >= 0.f) ? A.inv_bk : 0.f;
+          if (valid && lead) csum += c;
+          break;
         case KGE_LOSS_LOGISTIC: {
-          const float ex = expf(s - sp);
-          c = ex / (1.f + ex);
-          if (valid && lead) { lsum += logf(1.f + ex); csum += c; }
+          const float ex = fast_exp(s - sp);
+          c = ex * __builtin_amdgcn_rcpf(1.f + ex);
+          if (valid && lead) csum += c;
         } break;
         case KGE_LOSS_BCE:
-          c = sigmoid(s) * A.inv_b;
-          if (valid && lead) lsum += log_sigmoid(-s);
+          c = fast_sigmoid(s) * A.inv_b;
           break;
         case KGE_LOSS_SANS: {
           const float z = valid ? A.temperature * s : -INFINITY;
           const float Mn = fmaxf(Mrun, lane_reduce<5, true>(z));
           if (Mn > Mrun) {   // wave-uniform: rescale everything accumulated so far
-            const float sc = (Mrun == -INFINITY) ? 0.f : expf(Mrun - Mn);
+            const float sc = (Mrun == -INFINITY) ? 0.f : fast_exp(Mrun - Mn);
             const float sc2 = sc * sc;
 #pragma unroll
             for (int q = 0; q < VEC * NC; ++q) { accH.v[q] *= sc; accR.v[q] *= sc; accT.v[q] *= sc; }
 #pragma unroll
             for (int v = 0; v < 4; ++v) nrm[v] *= sc2;
             Zs *= sc;
-            lsum *= sc;
             Mrun = Mn;
           }
-          const float e = valid ? expf(z - Mrun) : 0.f;
-          c = e * sigmoid(s + A.margin) * A.inv_b;
-          if (valid && lead) { Zs += e; lsum += e * log_sigmoid(-s - A.margin); }
+          const float e = valid ? fast_exp(z - Mrun) : 0.f;
+          c = e * fast_sigmoid(s + A.margin) * A.inv_b;
+          if (valid && lead) Zs += e;
         } break;
         default:  // SQERR
           c = s * A.inv_b;
-          if (valid && lead) lsum += s * s;
           break;
       }
-      const float al = valid ? score_alpha<SK>(c, Rl, lp, tl, A.pw) : 0.f;
-      if (valid && lead) { gR[j] = Rl; gT[j] = tl; }
-#pragma unroll
-      for (int u = 0; u < ROWS; ++u) {
-        if (j0 + u < jend) {
-          const float alu = bcast(al, u << SH);
-          const float Mu = SK == SK_PINF ? bcast(Rl, u << SH) : 0.f;
-          const int kind = slot_kind(A.side_mode, j0 + u);
-          F a, b;
-          M::fwd(ctx, kind, E[u], a, b);
-          M::bwd(ctx, kind, E[u], a, b, alu, Mu, accH, accR, accT, nrm, mp);
+      const float al = valid ? score_alpha_fast<SK>(c, Rl, lp, tl, A.pw) : 0.f;
+      if (valid && lead) {
+        gR[j] = Rl;
+        gT[j] = tl;
+        if (M::NRM_FROM_R) {   // ||alpha a||^2 = alpha^2 R: h- and t-lookup slices, r-lookup slice
+          const float n2 = al * al * Rl;
+          nrm[0] += 2.f * n2;
+          nrm[1] += n2;
         }
       }
+      // backward: rows past the range carry alpha = 0
+      static_for<ROWS>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        const float alu = bcast(al, u << SH);
+        const float Mu = SK == SK_PINF ? bcast(Rl, u << SH) : 0.f;
+        M::template bwdk<kind_at<SIDE>(u)>(ctx, E[u], a[u], b[u], alu, Mu, accH, accR, accT, nrm, mp);
+      });
     }
+    M::finish(accH, accR, accT);
   }
   KGE_PROF(1);
 
   // ---- wave state -> LDS
   {
-    const float Zw = wave_sum(Zs), lw = wave_sum(lsum), cw = wave_sum(csum);
+    const float Zw = wave_sum(Zs), cw = wave_sum(csum);
     float nw[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) nw[v] = wave_sum(nrm[v]);
     if (lane == 0) {
       float* st = s_st + wv * 8;
-      st[0] = Mrun; st[1] = Zw; st[2] = lw; st[3] = cw;
+      st[0] = Mrun; st[1] = Zw; st[2] = 0.f; st[3] = cw;
       st[4] = nw[0]; st[5] = nw[1]; st[6] = nw[2]; st[7] = nw[3];
     }
     if (A.train) {
@@ -529,16 +560,16 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
     float Ms = -INFINITY;
     for (int g = 0; g < wpp; ++g) Ms = fmaxf(Ms, st[g * 8]);
     float f[kMaxWpp];
-    float Z = 0.f, lw = 0.f, cw = 0.f;
+    float Z = 0.f, cw = 0.f;
     for (int g = 0; g < wpp; ++g) {
       const float sc = !sans ? 1.f : (st[g * 8] == -INFINITY ? 0.f : expf(st[g * 8] - Ms));
       f[g] = sc;
       Z += st[g * 8 + 1] * sc;
-      lw += st[g * 8 + 2] * sc;
       cw += st[g * 8 + 3];
     }
     const float invZ = sans ? (Z > 0.f ? 1.f / Z : 0.f) : 1.f;
-    lw *= invZ;
+    // the positive's own loss terms; the negatives' sums come from the finalise pass
+    const float lw = 0.f;
     const float Rpv = mg[MG_RP], tpv = mg[MG_TP], spv = mg[MG_SP], lppv = mg[MG_LPP];
     float lossp, cp;
     switch (A.loss_kind) {
@@ -605,8 +636,10 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
     }
   }
 
-  // ---- each wave finalises its slots: coefficient, score, destination key
-  if (active && (A.train || A.neg_score_out)) {
+  // ---- each wave finalises its slots: loss terms, coefficient, score,
+  // destination key (one lane per slot, IEEE transcendentals)
+  float lfin = 0.f;
+  if (active) {
     const float* mg = s_mrg + grp * MG_STRIDE;
     const float Ms = mg[MG_MS], invZ = mg[MG_IZ], spv = mg[MG_SP];
     for (int j = jbeg + lane; j < jend; j += KGE_WAVE) {
@@ -614,6 +647,13 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
       float lp;
       const float s = score_value<SK>(R, A.pw, &lp);
       const int64_t q = i * Keff + j;
+      switch (A.loss_kind) {
+        case KGE_LOSS_HINGE: lfin += fmaxf(A.margin + s - spv, 0.f); break;
+        case KGE_LOSS_LOGISTIC: lfin += logf(1.f + expf(s - spv)); break;
+        case KGE_LOSS_BCE: lfin += log_sigmoid(-s); break;
+        case KGE_LOSS_SANS: lfin += expf(A.temperature * s - Ms) * invZ * log_sigmoid(-s - A.margin); break;
+        default: lfin += s * s; break;
+      }
       if (A.neg_score_out) A.neg_score_out[q] = s;
       if (A.train) {
         const float c = neg_coef(A, s, spv, Ms, invZ);
@@ -622,6 +662,8 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
       }
     }
   }
+  lfin = wave_sum(lfin);
+  if (lane == 0) s_st[wv * 8 + 2] = lfin;   // (merge state already consumed)
   if (A.train && tid < nValid * 3) {
     const int p = tid / 3, c = tid % 3;
     const int64_t dest = c == 0 ? s_pos[p * 3] : c == 1 ? s_pos[p * 3 + 2] : A.ent.rows + s_pos[p * 3 + 1];
@@ -629,14 +671,24 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
   }
   if (err) set_status(A.status, err);
   KGE_PROF(4);
+  __syncthreads();
 
   // ---- workgroup partials; the last workgroup to finish reduces them in a
   // fixed order and publishes the clip scales and the loss
   if (tid == 0) {
+    float wl;   // weight of a wave's summed negative loss terms (loss.py)
+    switch (A.loss_kind) {
+      case KGE_LOSS_HINGE: wl = A.inv_bk; break;
+      case KGE_LOSS_LOGISTIC: wl = 1.f; break;
+      case KGE_LOSS_SANS: case KGE_LOSS_BCE: wl = -A.inv_b; break;
+      default: wl = 0.5f * A.inv_b; break;
+    }
     float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
     for (int p = 0; p < nValid; ++p) {
       const float* mg = s_mrg + p * MG_STRIDE;
-      acc[0] += mg[MG_LOSS];
+      float lneg = 0.f;
+      for (int g = 0; g < wpp; ++g) lneg += s_st[(p * wpp + g) * 8 + 2];
+      acc[0] += mg[MG_LOSS] + wl * lneg;
 #pragma unroll
       for (int v = 0; v < 4; ++v) acc[1 + v] += mg[MG_N + v];
     }
@@ -883,7 +935,20 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
 // ------------------------------------------------------------ dispatch
 template <template <int, int, int> class Model, int VEC, int NC, int SK>
 static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_t st, hipEvent_t const* ev) {
-  hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK>), dim3(G.nWG), dim3(kStepThreads), G.lds_score, st, A);
+#ifdef KGE_ONLY_ONE
+  hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK, KGE_SIDE_HT>), dim3(G.nWG), dim3(kStepThreads), G.lds_score,
+                     st, A);
+#else
+  if (A.side_mode == KGE_SIDE_HT)
+    hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK, KGE_SIDE_HT>), dim3(G.nWG), dim3(kStepThreads), G.lds_score,
+                       st, A);
+  else if (A.side_mode == KGE_SIDE_H)
+    hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK, KGE_SIDE_H>), dim3(G.nWG), dim3(kStepThreads), G.lds_score,
+                       st, A);
+  else
+    hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK, KGE_SIDE_T>), dim3(G.nWG), dim3(kStepThreads), G.lds_score,
+                       st, A);
+#endif
   if (ev) (void)hipEventRecord(ev[2], st);
   if (A.train)
     hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
@@ -954,7 +1019,7 @@ kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int mod
                                    hipStream_t st, hipEvent_t const* ev) {
 #ifdef KGE_ONLY_ONE
   // quick-iteration builds (tools/phase_prof.py): the bench's C2 instance only
-  if (model == KGE_MODEL_TRANSE && G.vec == 4 && G.nc == 1 && sk == SK_P2)
+  if (model == KGE_MODEL_TRANSE && G.vec == 4 && G.nc == 1 && sk == SK_P2 && A.side_mode == KGE_SIDE_HT)
     return launch_family<TransE, 4, 1, SK_P2>(A, G, st, ev);
   return KGE_EUNSUPPORTED;
 #else

@@ -21,20 +21,20 @@ for p in (ROOT, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 CSRC = os.path.join(PKG, "csrc")
-LIB = os.path.join(PKG, "KGE", "_lib", "libkge_hip_prof.so")
+LIB = os.path.join(PKG, "KGE", "_lib", os.environ.get("KGE_PROF_LIB", "libkge_hip_prof.so"))
 
 SCORE_PHASES = {0: "ids+sample", 1: "ctx+stream (gather/fwd/reduce/bwd)", 2: "wave state->LDS", 3: "merge",
                 4: "gpos+finalize+bin", 5: "partials+last-WG reduce"}
 UPDATE_PHASES = {16: "dest rows (sort+sum+apply)"}
 
 
-def build():
+def build(extra=()):
     objs = []
     for src in ("kge_step.hip", "kge_abi.hip"):
         obj = os.path.join("/tmp", "prof_" + src.replace(".hip", ".o"))
         # the bench's instance only (KGE_ONLY_ONE): seconds instead of minutes
         subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DKGE_PHASE_PROF",
-                        "-DKGE_ONLY_ONE", "-c", os.path.join(CSRC, src), "-o", obj], check=True)
+                        "-DKGE_ONLY_ONE"] + list(extra) + ["-c", os.path.join(CSRC, src), "-o", obj], check=True)
         objs.append(obj)
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", LIB], check=True)
     print("built", LIB)
@@ -97,4 +97,4 @@ if __name__ == "__main__":
     ap.add_argument("--score-wgs", type=int, default=0)
     ap.add_argument("--update-wgs", type=int, default=3686)
     a = ap.parse_args()
-    build() if a.cmd == "build" else run(a)
+    build(os.environ.get("KGE_PROF_FLAGS", "").split()) if a.cmd == "build" else run(a)
