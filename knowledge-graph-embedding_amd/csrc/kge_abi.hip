@@ -152,7 +152,14 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   const int64_t E = d->ent.rows, R = d->rel.rows;
   const int64_t ndest = E + R;
   const int64_t T = B * (Keff + 3);
-  if (T >= (int64_t)0xFFFFFFFF) return fail(KGE_EUNSUPPORTED, "batch * (negative_ratio + 3) exceeds 2^32 keys");
+  // destination codes: (i << kshift) | j for slot j of positive i, then
+  // (B << kshift) + 4 i + c for the positive's own rows (shift-decoded)
+  int kshift = 0;
+  while ((1LL << kshift) < Keff) ++kshift;
+  if ((B << kshift) + 4 * B >= (int64_t)0xFFFFFFFF)
+    return fail(KGE_EUNSUPPORTED, "batch x negative_ratio too large for 32-bit destination codes");
+  if (B * 3 * std::max(entc, relc) >= (int64_t)0xFFFFFFFF)
+    return fail(KGE_EUNSUPPORTED, "batch x embedding size too large for 32-bit context offsets");
   // per-destination list capacity: ~4x the mean load, 64..256 entries (the
   // update kernel orders up to 256 in registers; longer lists overflow)
   int64_t cap = 64;
@@ -204,7 +211,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.SW = SW;
   A.nWG = (int32_t)nWG;
   A.cap = (int32_t)cap;
-  A.nkeyneg = (uint32_t)(B * Keff);
+  A.kshift = kshift;
+  A.nkeyneg = (uint32_t)(B << kshift);
   A.snap_cols = (int32_t)entc;
   A.gcols = (int32_t)rowlen;
   A.rel_gcols = (int32_t)relc;
@@ -221,7 +229,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   // zero-state words first: control block, per-destination counters
   P.o_ctl = take(sizeof(StepCtl));
   P.o_cnt = take((uint64_t)ndest * 4);
-  P.o_coef = take((uint64_t)B * Keff * 8);
+  P.o_coef = take((uint64_t)(B << kshift) * 8);   // indexed by destination code
   P.o_snap = take((uint64_t)B * nsnap * entc * 4);
   P.o_gpos = take((uint64_t)B * 3 * rowlen * 4);
   P.o_part = take((uint64_t)nWG * 8 * 4);

@@ -263,6 +263,14 @@ struct TransE {
   // accH - accT. P2: the row gradient is alpha * a, so its norm^2 is
   // alpha^2 * R, accumulated from the reduced value (NRM_FROM_R).
   static constexpr bool NRM_FROM_R = SK == SK_P2;
+  // update kernel: P2 negative gradient wrt its entity row E is
+  // alpha (E + D) (h-corrupted) or alpha (E - X) (t-corrupted); Dot: alpha c0
+  static constexpr bool LINEAR_E = SK == SK_P2 || SK == SK_DOT;
+  __device__ static void lin_coefs(int kind, float alpha, float& aE, float& aC) {
+    if (SK == SK_DOT) { aE = 0.f; aC = alpha; return; }
+    aE = alpha;
+    aC = kind == KIND_HC ? alpha : -alpha;
+  }
   template <int KIND>
   __device__ static void fwdk(const Ctx& c, const F& E, F& a, F& b) {
 #pragma unroll
@@ -385,6 +393,9 @@ struct DistMult {
   }
   // score-kernel stream hooks: slot kind known at compile time
   static constexpr bool NRM_FROM_R = false;   // row-gradient norm^2 from the reduced value
+  // update kernel: a negative's entity gradient is aE * E + aC * c0 (scalars)
+  static constexpr bool LINEAR_E = true;    // gradient wrt the entity row is alpha * c0
+  __device__ static void lin_coefs(int kind, float alpha, float& aE, float& aC) { aE = 0.f; aC = alpha; }
   template <int KIND>
   __device__ static void fwdk(const Ctx& c, const F& E, F& a, F& b) { fwd(c, KIND, E, a, b); }
   template <int KIND>
@@ -481,6 +492,9 @@ struct RotatE {
   }
   // score-kernel stream hooks: slot kind known at compile time
   static constexpr bool NRM_FROM_R = false;   // row-gradient norm^2 from the reduced value
+  // update kernel: a negative's entity gradient is aE * E + aC * c0 (scalars)
+  static constexpr bool LINEAR_E = false;
+  __device__ static void lin_coefs(int kind, float alpha, float& aE, float& aC) { aE = 0.f; aC = alpha; }
   template <int KIND>
   __device__ static void fwdk(const Ctx& c, const F& E, F& a, F& b) { fwd(c, KIND, E, a, b); }
   template <int KIND>

@@ -55,7 +55,8 @@ struct StepArgs {
   int32_t nWG;      // score workgroups
   int32_t cap;      // destination list capacity (entries per destination)
   int32_t snap_cols, gcols, rel_gcols;
-  uint32_t nkeyneg; // B * Keff: codes below are negatives (i * Keff + j), above positive rows
+  uint32_t nkeyneg; // B << kshift: codes below are negatives (i << kshift | j), above positive rows (+4i+c)
+  int32_t kshift;   // log2 of the slot stride (next power of two >= Keff)
   // workspace
   StepCtl* ctl;
   float2* coef;     // [B*Keff] (alpha, reduced value) per negative

@@ -33,6 +33,9 @@
 #ifndef KGE_STREAM_ROWS
 #define KGE_STREAM_ROWS 8   // sampled rows per stream batch at NC = 1 (tuning knob)
 #endif
+#ifndef KGE_UPDATE_U
+#define KGE_UPDATE_U 8      // update kernel: list entries in flight per wave at NC = 1 (tuning knob)
+#endif
 
 namespace kge {
 
@@ -657,8 +660,8 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
       if (A.neg_score_out) A.neg_score_out[q] = s;
       if (A.train) {
         const float c = neg_coef(A, s, spv, Ms, invZ);
-        A.coef[q] = make_float2(score_alpha<SK>(c, R, lp, gT[j], A.pw), R);
-        bin_key(A, ids[j], (uint32_t)q);
+        A.coef[((uint32_t)i << A.kshift) | (uint32_t)j] = make_float2(score_alpha<SK>(c, R, lp, gT[j], A.pw), R);
+        bin_key(A, ids[j], ((uint32_t)i << A.kshift) | (uint32_t)j);
       }
     }
   }
@@ -667,7 +670,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
   if (A.train && tid < nValid * 3) {
     const int p = tid / 3, c = tid % 3;
     const int64_t dest = c == 0 ? s_pos[p * 3] : c == 1 ? s_pos[p * 3 + 2] : A.ent.rows + s_pos[p * 3 + 1];
-    bin_key(A, dest, A.nkeyneg + (uint32_t)(3 * (i0 + p) + c));
+    bin_key(A, dest, A.nkeyneg + (((uint32_t)(i0 + p)) << 2) + (uint32_t)c);
   }
   if (err) set_status(A.status, err);
   KGE_PROF(4);
@@ -752,7 +755,7 @@ template <template <int, int, int> class Model, int VEC, int NC, int SK>
 __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
   using M = Model<VEC, NC, SK>;
   using F = Frag<VEC, NC>;
-  constexpr int U = NC == 1 ? 8 : NC == 2 ? 4 : 2;   // entries in flight per wave
+  constexpr int U = KGE_UPDATE_U / NC > 1 ? KGE_UPDATE_U / NC : 2;   // entries in flight per wave
   constexpr int RV = RelV<M::CPLX, VEC>::n;
   constexpr int CHMAX = 4;                            // in-register ordering up to 256 codes
   __shared__ uint32_t s_scr[kUpdWaves][CHMAX * KGE_WAVE];
@@ -761,24 +764,30 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
   const int lane = lane_id(), wv = wave_id();
   const int64_t E_ = A.ent.rows;
   const int64_t ndest = E_ + A.rel.rows;
-  const int64_t d = (int64_t)blockIdx.x * kUpdWaves + wv;
+  // relation rows first: few rows with the longest lists (every positive
+  // files one), so they start early instead of forming the kernel's tail
+  const int64_t R_ = A.rel.rows;
+  const int64_t dd = (int64_t)blockIdx.x * kUpdWaves + wv;
+  const int64_t d = dd < R_ ? E_ + dd : dd - R_;
   const uint32_t nneg = A.nkeyneg;
+  const uint32_t kmask = (1u << A.kshift) - 1u;
+  const uint32_t snap_stride = (uint32_t)(M::NSNAP * A.snap_cols);   // B * stride < 2^32 (plan check)
+  const float sc_ent = A.ctl->scale[0], sc_rel = A.ctl->scale[1];   // issued up front
 
   // one code -> its positive i and slot j (negative, c = -1) or row part c (0 h, 1 t, 2 r)
   auto decode = [&](uint32_t code, int64_t* i, int* j, int* c) {
     if (code < nneg) {
-      const uint32_t q = code / (uint32_t)A.Keff;
-      *i = q;
-      *j = (int)(code - q * (uint32_t)A.Keff);
+      *i = code >> A.kshift;
+      *j = (int)(code & ((1u << A.kshift) - 1u));
       *c = -1;
     } else {
-      const uint32_t q = (code - nneg) / 3u;
-      *i = q;
+      *i = (code - nneg) >> 2;
       *j = 0;
-      *c = (int)(code - nneg - q * 3u);
+      *c = (int)((code - nneg) & 3u);
     }
   };
   // entity destination: add the gradient rows of `cntv` (<= U) entries
+  float accE = 0.f;   // LINEAR_E models: summed coefficient of the destination row itself
   auto entity_add = [&](const uint32_t* codes, int cntv, const F& E, F& acc) {
     int64_t ii[U];
     int jj[U], cc[U];
@@ -789,7 +798,7 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
       if (u < cntv) {
         decode(codes[u], &ii[u], &jj[u], &cc[u]);
         if (cc[u] < 0) {
-          cf[u] = A.coef[ii[u] * A.Keff + jj[u]];
+          cf[u] = A.coef[codes[u]];
           M::load_ectx(A.snap + ii[u] * (M::NSNAP * (int64_t)A.snap_cols), A.snap_cols,
                        slot_kind(A.side_mode, jj[u]), ec[u]);
         } else {
@@ -802,9 +811,18 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
     for (int u = 0; u < U; ++u) {
       if (u < cntv) {
         if (cc[u] < 0) {
-          F g;
-          M::grad_entity(ec[u], slot_kind(A.side_mode, jj[u]), E, cf[u].x, cf[u].y, g);
-          add_to(acc, g);
+          if constexpr (M::LINEAR_E) {
+            // g = alpha_E * E + alpha_C * c0: wave-uniform scalars, one FMA per element
+            float aE, aC;
+            M::lin_coefs(slot_kind(A.side_mode, jj[u]), cf[u].x, aE, aC);
+            accE += aE;
+#pragma unroll
+            for (int q = 0; q < VEC * NC; ++q) acc.v[q] += aC * ec[u].c0.v[q];
+          } else {
+            F g;
+            M::grad_entity(ec[u], slot_kind(A.side_mode, jj[u]), E, cf[u].x, cf[u].y, g);
+            add_to(acc, g);
+          }
         } else {
           add_to(acc, ec[u].c0);
         }
@@ -830,21 +848,78 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
       }
   };
 
-  if (d < ndest) {
+  if (dd < ndest) {
+    const bool is_ent = d < E_;
+    const uint32_t* lst = A.list + d * (int64_t)A.cap;
+    // issued together: the counter, the list's first 64 entries (speculative;
+    // lanes past the count are ignored) and the entity row
     const uint32_t n = A.cnt[d];
+    const uint32_t code0 = lst[min(lane, A.cap - 1)];
+    F E, acc;
+    acc.zero();
+    E.zero();
+    if (is_ent) load_row(E, A.ent.row(d), A.ent.cols);
     if (n != 0u) {
       if (lane == 0) A.cnt[d] = 0u;   // ready for the next step
-      const bool is_ent = d < E_;
-      F E, acc;
-      acc.zero();
-      E.zero();
       float racc[RV * NC];
 #pragma unroll
       for (int q = 0; q < RV * NC; ++q) racc[q] = 0.f;
-      if (is_ent) load_row(E, A.ent.row(d), A.ent.cols);
-      const uint32_t* lst = A.list + d * (int64_t)A.cap;
-      if (n <= (uint32_t)A.cap && n <= (uint32_t)(CHMAX * KGE_WAVE)) {
-        // ascending code order: each code's rank among the n (codes are unique)
+      auto consume_sorted = [&](auto code_at) {
+        int p0 = 0;
+        if constexpr (M::LINEAR_E) {
+          if (is_ent) {
+            // the negatives come first in code order: U-wide batches with no
+            // per-entry branches (padding entries repeat a code with weight 0)
+            int nn = 0;   // negatives among the n codes (binary search on the sorted codes)
+            {
+              int lo = 0, hi = (int)n;
+              while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (code_at(mid) < nneg) lo = mid + 1; else hi = mid;
+              }
+              nn = lo;
+            }
+            for (; p0 < nn; p0 += U) {
+              typename M::ECtx ec[U];
+              float2 cf[U];
+              int kd[U];
+#pragma unroll
+              for (int u = 0; u < U; ++u) {
+                const uint32_t code = code_at(min(p0 + u, nn - 1));
+                const uint32_t i = code >> A.kshift;
+                kd[u] = slot_kind(A.side_mode, (int)(code & kmask));
+                cf[u] = A.coef[code];
+                M::load_ectx(A.snap + i * snap_stride, A.snap_cols, kd[u], ec[u]);
+              }
+#pragma unroll
+              for (int u = 0; u < U; ++u) {
+                float aE, aC;
+                M::lin_coefs(kd[u], p0 + u < nn ? cf[u].x : 0.f, aE, aC);
+                accE += aE;
+#pragma unroll
+                for (int q = 0; q < VEC * NC; ++q) acc.v[q] += aC * ec[u].c0.v[q];
+              }
+            }
+            p0 = nn;
+          }
+        }
+        for (; p0 < (int)n; p0 += U) {
+          uint32_t cs[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) cs[u] = code_at(min(p0 + u, (int)n - 1));
+          if (is_ent) entity_add(cs, min(U, (int)n - p0), E, acc);
+          else rel_add(cs, min(U, (int)n - p0), racc);
+        }
+      };
+      if (n <= (uint32_t)A.cap && n <= (uint32_t)KGE_WAVE) {
+        // ascending code order: each code's rank among the n (codes are
+        // unique), then a forward permute puts code of rank r in lane r
+        const uint32_t code = lane < (int)n ? code0 : 0xFFFFFFFFu;
+        uint32_t rank = 0u;
+        for (int q = 0; q < (int)n; ++q) rank += ((uint32_t)__builtin_amdgcn_readlane((int)code, q) < code) ? 1u : 0u;
+        const int sorted = __builtin_amdgcn_ds_permute((int)(min(rank, 63u) << 2), (int)code);
+        consume_sorted([&](int p) { return (uint32_t)__builtin_amdgcn_readlane(sorted, p); });
+      } else if (n <= (uint32_t)A.cap && n <= (uint32_t)(CHMAX * KGE_WAVE)) {
         const int nch = (int)((n + KGE_WAVE - 1) / KGE_WAVE);
         uint32_t code[CHMAX];
 #pragma unroll
@@ -871,13 +946,7 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int p0 = 0; p0 < (int)n; p0 += U) {
-          uint32_t cs[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) cs[u] = (uint32_t)__builtin_amdgcn_readfirstlane((int)scr[min(p0 + u, (int)n - 1)]);
-          if (is_ent) entity_add(cs, min(U, (int)n - p0), E, acc);
-          else rel_add(cs, min(U, (int)n - p0), racc);
-        }
+        consume_sorted([&](int p) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)scr[p]); });
       } else {
         // a list past its capacity: repeated selection of the next code from
         // the list and the overflow entries (correct for any skew, not fast)
@@ -906,12 +975,15 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
         }
       }
       if (is_ent) {
+        if constexpr (M::LINEAR_E) {
+#pragma unroll
+          for (int q = 0; q < VEC * NC; ++q) acc.v[q] += accE * E.v[q];
+        }
         if (A.grad_mode) {
           store_row(acc, A.gent + d * (int64_t)A.ent.cols, A.ent.cols);
         } else {
-          const float sc = A.ctl->scale[0];
 #pragma unroll
-          for (int q = 0; q < VEC * NC; ++q) E.v[q] = E.v[q] + acc.v[q] * sc;
+          for (int q = 0; q < VEC * NC; ++q) E.v[q] = E.v[q] + acc.v[q] * sc_ent;
           store_row(E, A.ent.row_w(d), A.ent.cols);
         }
       } else {
@@ -921,9 +993,8 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
         } else {
           float row[RV * NC];
           load_rel_row<M::CPLX, VEC, NC>(row, A.rel.row(r), A.rel.cols);
-          const float sc = A.ctl->scale[1];
 #pragma unroll
-          for (int q = 0; q < RV * NC; ++q) row[q] = row[q] + racc[q] * sc;
+          for (int q = 0; q < RV * NC; ++q) row[q] = row[q] + racc[q] * sc_rel;
           store_rel_row<M::CPLX, VEC, NC>(row, A.rel.row_w(r), A.rel.cols);
         }
       }

@@ -14,5 +14,5 @@ timeout -k 10 300 python -u bench.py --no-cpu-baseline > "$OUT/bench.json" 2> "$
 cat "$OUT/bench.json"
 if [ -f knowledge-graph-embedding_amd/KGE/_lib/libkge_hip_prof16.so ]; then
   KGE_PROF_LIB=libkge_hip_prof16.so timeout -k 10 200 python -u tools/phase_prof.py run --score-wgs 512 --update-wgs 3686 > "$OUT/phase16.txt" 2>&1 || { tail -20 "$OUT/phase16.txt"; exit 7; }
-  echo "== 16-row batches"; cat "$OUT/phase16.txt"
+  echo "== variant (U=16)"; cat "$OUT/phase16.txt"
 fi
