@@ -102,8 +102,10 @@ enum { KGE_OPT_NONE = 0, KGE_OPT_SGD = 1, KGE_OPT_GRAD = 2, KGE_OPT_ADAM = 3 };
 enum {
   KGE_FLAG_NO_TABLE_CONSTRAINT = 1, /* caller already applied the full-table
                                        _constraint_loss assigns (e.g. on its shard) */
-  KGE_FLAG_DEBUG_LIST_CAP = 2       /* test hook: 4-entry destination lists, so the
+  KGE_FLAG_DEBUG_LIST_CAP = 2,      /* test hook: 4-entry destination lists, so the
                                        update kernel's overflow path runs */
+  KGE_FLAG_DEBUG_UNFUSED_CONSTRAINT = 4 /* test hook: run the full-table renormalisation
+                                       as its own kernel even on the SGD path */
 };
 
 typedef struct kge_table {

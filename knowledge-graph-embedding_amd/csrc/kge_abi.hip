@@ -184,6 +184,12 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.i64 = d->idx_dtype == KGE_IDX_I64;
   A.train = d->optimizer != KGE_OPT_NONE;
   A.grad_mode = d->optimizer == KGE_OPT_GRAD;
+  // every entity row is renormalised by the step itself: rows on the stream
+  // as they are loaded, every row again (bit-identically) by the update
+  // kernel, which writes the normalised row plus this step's SGD delta
+  A.fuse_norm = d->optimizer == KGE_OPT_SGD && d->constraint && !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT) &&
+                (model == KGE_MODEL_TRANSE || model == KGE_MODEL_DISTMULT) &&
+                !(d->flags & KGE_FLAG_DEBUG_UNFUSED_CONSTRAINT);
   A.gent = d->grad_out[0];
   A.grel = d->grad_out[1];
   A.given = sm.kind == KGE_SAMPLER_GIVEN;
@@ -351,10 +357,11 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     (void)hipMemsetAsync(d->grad_out[0], 0, (size_t)A.ent.rows * A.ent.cols * sizeof(float), st);
     (void)hipMemsetAsync(d->grad_out[1], 0, (size_t)A.rel.rows * A.rel_gcols * sizeof(float), st);
   }
-  // _constraint_loss assigns before scoring (BaseModel.py:319)
+  // _constraint_loss assigns before scoring (BaseModel.py:319): fused into
+  // the score / update kernels on the SGD path (A.fuse_norm), else K0
   const bool renorm = d->constraint && !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT) &&
                       (d->model == KGE_MODEL_TRANSE || d->model == KGE_MODEL_DISTMULT);
-  if (renorm) {
+  if (renorm && !(A.fuse_norm && d->batch > 0)) {
     const int64_t blocks = std::min<int64_t>(ceil_div(d->ent.rows, kWaves), 4096);
     hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, d->ent.data,
                        d->ent.rows, (int32_t)d->ent.cols, d->ent.ld, 0, 1.0f);

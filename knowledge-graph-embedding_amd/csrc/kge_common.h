@@ -123,6 +123,90 @@ __device__ __forceinline__ float wave_max(float x) {
   return x;
 }
 
+// ------------------------------------------------------------ cross-lane
+// Lane pairings used by the reductions. Bits 5 and 4 go through the gfx950
+// half-exchange instructions (v_permlane32_swap / v_permlane16_swap); bits
+// 3..0 through DPP: row_mirror (l ^ 15), row_half_mirror (l ^ 7),
+// quad_perm [2,3,0,1] (l ^ 2), quad_perm [1,0,3,2] (l ^ 1). Each pairing
+// flips lane bit B, and together they span all 64 lanes.
+template <int B> struct PairCtl;
+template <> struct PairCtl<3> { static constexpr int v = 0x140; };
+template <> struct PairCtl<2> { static constexpr int v = 0x141; };
+template <> struct PairCtl<1> { static constexpr int v = 0x4E; };
+template <> struct PairCtl<0> { static constexpr int v = 0xB1; };
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+template <bool MAX>
+__device__ __forceinline__ float comb(float a, float b) { return MAX ? fmaxf(a, b) : a + b; }
+
+// half exchange across lane bit B (5 or 4): lo = a with the high side's a
+// moved in, hi = b with the low side's b moved in (v_permlane{32,16}_swap)
+template <int B>
+__device__ __forceinline__ void half_swap(float a, float b, float& lo, float& hi) {
+  const unsigned ua = __builtin_bit_cast(unsigned, a), ub = __builtin_bit_cast(unsigned, b);
+  if constexpr (B == 5) {
+    const auto r = __builtin_amdgcn_permlane32_swap(ua, ub, false, false);
+    lo = __builtin_bit_cast(float, (unsigned)r[0]);
+    hi = __builtin_bit_cast(float, (unsigned)r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(ua, ub, false, false);
+    lo = __builtin_bit_cast(float, (unsigned)r[0]);
+    hi = __builtin_bit_cast(float, (unsigned)r[1]);
+  }
+}
+
+// all-lane reduction of one value over lane bits [0, B]
+template <int B, bool MAX>
+__device__ __forceinline__ float lane_reduce(float v) {
+  if constexpr (B < 0) {
+    return v;
+  } else {
+    if constexpr (B >= 4) {
+      float x, y;
+      half_swap<B>(v, v, x, y);
+      v = comb<MAX>(x, y);
+    } else {
+      v = comb<MAX>(v, dpp_mov<PairCtl<B>::v>(v));
+    }
+    return lane_reduce<B - 1, MAX>(v);
+  }
+}
+
+// Transposed multi-reduction: N per-lane partials (N a power of two <= 64)
+// -> lane l holds the wave-wide reduction of value (l >> (6 - log2 N)).
+// Each step halves the list: a lane keeps one half, sends the other to its
+// partner and adds what it receives, so N values cost N - 1 + (6 - log2 N)
+// exchanges instead of 6 N.
+template <int N, bool MAX, int B = 5>
+__device__ __forceinline__ float multi_reduce(const float (&x)[N]) {
+  if constexpr (N == 1) {
+    return lane_reduce<B, MAX>(x[0]);
+  } else {
+    constexpr int H = N / 2;
+    float y[H];
+    if constexpr (B >= 4) {
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        float lo, hi;
+        half_swap<B>(x[k], x[H + k], lo, hi);
+        y[k] = comb<MAX>(lo, hi);
+      }
+    } else {
+      const bool up = (lane_id() >> B) & 1;
+#pragma unroll
+      for (int k = 0; k < H; ++k) {
+        const float keep = up ? x[H + k] : x[k];
+        const float send = up ? x[k] : x[H + k];
+        y[k] = comb<MAX>(keep, dpp_mov<PairCtl<B>::v>(send));
+      }
+    }
+    return multi_reduce<H, MAX, B - 1>(y);
+  }
+}
+
 // ---------------------------------------------------------------- fragments
 template <int VEC, int NC>
 struct Frag {
@@ -248,6 +332,31 @@ extern __device__ unsigned long long g_kge_prof[64];
 #define KGE_PROF_INIT() do {} while (0)
 #define KGE_PROF(k) do {} while (0)
 #endif
+
+// Row normalisation of the fused constraint (TransE.py:171-172,
+// DistMult.py:162-163: X / pow(sum |X|^2, 1/2) * 1): the per-lane partial is
+// rounded op by op (no contraction) and reduced with lane_reduce's tree, the
+// same tree multi_reduce uses, so every kernel that normalises a row gets the
+// same bits. Lanes past the row's end must hold zeros.
+template <int VEC, int NC>
+__device__ __forceinline__ float norm_partial(const Frag<VEC, NC>& f) {
+#pragma clang fp contract(off)
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VEC * NC; ++i) s = s + f.v[i] * f.v[i];
+  return s;
+}
+__device__ __forceinline__ float inv_norm(float sumsq) { return 1.f / sqrtf(sumsq); }
+template <int VEC, int NC>
+__device__ __forceinline__ void scale_row(Frag<VEC, NC>& f, float k) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int i = 0; i < VEC * NC; ++i) f.v[i] = f.v[i] * k;
+}
+template <int VEC, int NC>
+__device__ __forceinline__ void normalize_row(Frag<VEC, NC>& f) {
+  scale_row(f, inv_norm(lane_reduce<5, false>(norm_partial(f))));
+}
 
 __device__ __forceinline__ void set_status(int32_t* status, int code) {
   if (status) atomicCAS(status, 0, code);

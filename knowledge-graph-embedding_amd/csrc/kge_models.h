@@ -187,6 +187,7 @@ struct TabView {
 // Model scalars shared by every policy call.
 struct MP {
   float limit;   // RotatE phase range (RotatE.py:93)
+  bool norm;     // fused full-table renormalisation: h / t context rows normalised on load
 };
 
 // Context rows ("snap") written per positive by the score kernel and read
@@ -212,11 +213,15 @@ struct TransE {
   struct ECtx { F c0; };
 
   __device__ static void load_ctx(Ctx& c, const TabView& ent, const TabView& rel, int64_t h,
-                                  int64_t r, int64_t t, const MP&) {
+                                  int64_t r, int64_t t, const MP& mp) {
     F H;
     load_row(H, ent.row(h), ent.cols);
     load_row(c.R, rel.row(r), rel.cols);
     load_row(c.T, ent.row(t), ent.cols);
+    if (mp.norm) {
+      normalize_row(H);
+      normalize_row(c.T);
+    }
 #pragma unroll
     for (int i = 0; i < VEC * NC; ++i) {
       c.X.v[i] = H.v[i] + c.R.v[i];
@@ -356,10 +361,14 @@ struct DistMult {
   struct ECtx { F c0; };
 
   __device__ static void load_ctx(Ctx& c, const TabView& ent, const TabView& rel, int64_t h,
-                                  int64_t r, int64_t t, const MP&) {
+                                  int64_t r, int64_t t, const MP& mp) {
     load_row(c.H, ent.row(h), ent.cols);
     load_row(c.R, rel.row(r), rel.cols);
     load_row(c.T, ent.row(t), ent.cols);
+    if (mp.norm) {
+      normalize_row(c.H);
+      normalize_row(c.T);
+    }
 #pragma unroll
     for (int i = 0; i < VEC * NC; ++i) {
       c.HR.v[i] = c.H.v[i] * c.R.v[i];

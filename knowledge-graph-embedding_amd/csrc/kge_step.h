@@ -35,6 +35,7 @@ struct StepArgs {
   bool pw;          // LpDistancePow
   bool rel_half;    // RotatE: relation row is the phase half-row
   bool grad_mode;   // KGE_OPT_GRAD: write summed gradients, no update
+  bool fuse_norm;   // _constraint_loss renormalisation fused into the step (SGD path)
   int64_t B;
   int32_t Keff;     // negatives per positive actually produced
   int32_t Kside;    // draws per side

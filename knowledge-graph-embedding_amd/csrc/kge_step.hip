@@ -130,90 +130,6 @@ __device__ __forceinline__ int slot_kind(int side_mode, int j) {
   return side_mode == KGE_SIDE_H ? KIND_HC : KIND_TC;
 }
 
-// ------------------------------------------------------------ cross-lane
-// Lane pairings used by the reductions. Bits 5 and 4 go through the gfx950
-// half-exchange instructions (v_permlane32_swap / v_permlane16_swap); bits
-// 3..0 through DPP: row_mirror (l ^ 15), row_half_mirror (l ^ 7),
-// quad_perm [2,3,0,1] (l ^ 2), quad_perm [1,0,3,2] (l ^ 1). Each pairing
-// flips lane bit B, and together they span all 64 lanes.
-template <int B> struct PairCtl;
-template <> struct PairCtl<3> { static constexpr int v = 0x140; };
-template <> struct PairCtl<2> { static constexpr int v = 0x141; };
-template <> struct PairCtl<1> { static constexpr int v = 0x4E; };
-template <> struct PairCtl<0> { static constexpr int v = 0xB1; };
-
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
-template <bool MAX>
-__device__ __forceinline__ float comb(float a, float b) { return MAX ? fmaxf(a, b) : a + b; }
-
-// half exchange across lane bit B (5 or 4): lo = a with the high side's a
-// moved in, hi = b with the low side's b moved in (v_permlane{32,16}_swap)
-template <int B>
-__device__ __forceinline__ void half_swap(float a, float b, float& lo, float& hi) {
-  const unsigned ua = __builtin_bit_cast(unsigned, a), ub = __builtin_bit_cast(unsigned, b);
-  if constexpr (B == 5) {
-    const auto r = __builtin_amdgcn_permlane32_swap(ua, ub, false, false);
-    lo = __builtin_bit_cast(float, (unsigned)r[0]);
-    hi = __builtin_bit_cast(float, (unsigned)r[1]);
-  } else {
-    const auto r = __builtin_amdgcn_permlane16_swap(ua, ub, false, false);
-    lo = __builtin_bit_cast(float, (unsigned)r[0]);
-    hi = __builtin_bit_cast(float, (unsigned)r[1]);
-  }
-}
-
-// all-lane reduction of one value over lane bits [0, B]
-template <int B, bool MAX>
-__device__ __forceinline__ float lane_reduce(float v) {
-  if constexpr (B < 0) {
-    return v;
-  } else {
-    if constexpr (B >= 4) {
-      float x, y;
-      half_swap<B>(v, v, x, y);
-      v = comb<MAX>(x, y);
-    } else {
-      v = comb<MAX>(v, dpp_mov<PairCtl<B>::v>(v));
-    }
-    return lane_reduce<B - 1, MAX>(v);
-  }
-}
-
-// Transposed multi-reduction: N per-lane partials (N a power of two <= 64)
-// -> lane l holds the wave-wide reduction of value (l >> (6 - log2 N)).
-// Each step halves the list: a lane keeps one half, sends the other to its
-// partner and adds what it receives, so N values cost N - 1 + (6 - log2 N)
-// exchanges instead of 6 N.
-template <int N, bool MAX, int B = 5>
-__device__ __forceinline__ float multi_reduce(const float (&x)[N]) {
-  if constexpr (N == 1) {
-    return lane_reduce<B, MAX>(x[0]);
-  } else {
-    constexpr int H = N / 2;
-    float y[H];
-    if constexpr (B >= 4) {
-#pragma unroll
-      for (int k = 0; k < H; ++k) {
-        float lo, hi;
-        half_swap<B>(x[k], x[H + k], lo, hi);
-        y[k] = comb<MAX>(lo, hi);
-      }
-    } else {
-      const bool up = (lane_id() >> B) & 1;
-#pragma unroll
-      for (int k = 0; k < H; ++k) {
-        const float keep = up ? x[H + k] : x[k];
-        const float send = up ? x[k] : x[H + k];
-        y[k] = comb<MAX>(keep, dpp_mov<PairCtl<B>::v>(send));
-      }
-    }
-    return multi_reduce<H, MAX, B - 1>(y);
-  }
-}
-
 __device__ __forceinline__ float bcast(float v, int lane) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
@@ -330,7 +246,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
   KGE_PROF_INIT();
   const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
   const int grp = wv / wpp, gw = wv % wpp;
-  const MP mp{A.limit};
+  const MP mp{A.limit, A.fuse_norm};
   int err = 0;
 
   const int64_t i0 = (int64_t)blockIdx.x * nP;
@@ -415,6 +331,16 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
         const float* row = A.ent.row(__builtin_amdgcn_readlane(idv, jo + min(u, nrow - 1)));
         if (RAW) load_row_raw(E[u], row, A.ent.cols);
         else load_row(E[u], row, A.ent.cols);
+      }
+      if (A.fuse_norm) {
+        // fused _constraint_loss: each sampled row normalised in registers
+        // (one transposed reduction for the batch; same tree as lane_reduce)
+        float sq[ROWS];
+#pragma unroll
+        for (int u = 0; u < ROWS; ++u) sq[u] = (!RAW || lane_in) ? norm_partial(E[u]) : 0.f;
+        const float inv = inv_norm(multi_reduce<ROWS, false>(sq));
+#pragma unroll
+        for (int u = 0; u < ROWS; ++u) scale_row(E[u], bcast(inv, u << SH));
       }
       F a[ROWS], b[ROWS];
       float part[ROWS];
@@ -858,7 +784,13 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
     F E, acc;
     acc.zero();
     E.zero();
-    if (is_ent) load_row(E, A.ent.row(d), A.ent.cols);
+    if (is_ent) {
+      load_row(E, A.ent.row(d), A.ent.cols);
+      if (A.fuse_norm) {
+        normalize_row(E);   // the step's constraint assign, then this step's update
+        if (n == 0u) store_row(E, A.ent.row_w(d), A.ent.cols);
+      }
+    }
     if (n != 0u) {
       if (lane == 0) A.cnt[d] = 0u;   // ready for the next step
       float racc[RV * NC];

@@ -69,9 +69,14 @@ def run(args):
         step(batches[s], True, opt)
     torch.cuda.synchronize()
     raw.kge_prof_read(buf, 64)
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    t0.record()
     for s in range(args.steps):
         step(batches[5 + s], True, opt)
+    t1.record()
     torch.cuda.synchronize()
+    print("step time (incl. profiling atomics): %.4f ms" % (t0.elapsed_time(t1) / args.steps))
     step.check_status()
     raw.kge_prof_read(buf, 64)
     ticks = list(buf)
