@@ -147,30 +147,44 @@ def main():
     torch.cuda.synchronize()
     step.check_status()
 
-    # per-kernel HIP events: [before K0, before KS, before KU, after KU] per step
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    for row in evs:
-        for e in row:
-            e.record()
-    torch.cuda.synchronize()
-    handles = [(ctypes.c_void_p * 4)(*[e.cuda_event for e in row]) for row in evs]
-
+    # timed region: exactly K steps, nothing else on the stream
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        step(batches[args.warmup + s], True, opt, prof_events=handles[s])
+        step(batches[args.warmup + s], True, opt)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     t1 = time.perf_counter()
     step.check_status()
-
     ms = (t1 - t0) * 1e3 / args.steps
+
+    # per-kernel breakdown for the roofline: a second pass over the same
+    # batches with HIP events recorded on the step's own stream between the
+    # kernels [before K0, before KS, before KU, after KU]; the events cost a
+    # few us per step, so this pass never feeds `value`
+    n_prof = min(args.steps, 100)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(n_prof)]
+    for row in evs:
+        for e in row:
+            e.record()
+    torch.cuda.synchronize()
+    handles = [(ctypes.c_void_p * 4)(*[e.cuda_event for e in row]) for row in evs]
+    for s in range(n_prof):
+        step(batches[args.warmup + s], True, opt, prof_events=handles[s])
+    torch.cuda.synchronize()
+    step.check_status()
     k0 = float(np.mean([r[0].elapsed_time(r[1]) for r in evs]))
     ks = float(np.mean([r[1].elapsed_time(r[2]) for r in evs]))
     ku = float(np.mean([r[2].elapsed_time(r[3]) for r in evs]))
+    # single-GPU SGD + constraint: the renormalisation is fused into KS / KU
+    # (no K0 launch; its event pair brackets nothing) and KU also reads and
+    # writes every entity row
+    fused = world == 1
+    if fused:
+        k0 = 0.0
     if world > 1:
         t = torch.tensor([ms], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -182,7 +196,9 @@ def main():
     step_b, score_b, upd_b, con_b = algorithmic_bytes(B, K, d, E)
     kern = {"constrain_rows_kernel": {"ms": k0, "alg_bytes": con_b},
             "score_kernel": {"ms": ks, "alg_bytes": score_b},
-            "update_kernel": {"ms": ku, "alg_bytes": upd_b}}
+            "update_kernel": {"ms": ku, "alg_bytes": upd_b + (con_b if fused else 0)}}
+    if fused:
+        del kern["constrain_rows_kernel"]
     for v in kern.values():
         v["GBps"] = v["alg_bytes"] / (v["ms"] * 1e-3) / 1e9
     dom = max(kern, key=lambda k: kern[k]["ms"])
