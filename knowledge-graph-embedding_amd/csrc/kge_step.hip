@@ -185,6 +185,27 @@ __device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_
   }
 }
 
+// slot j of positive i: its entity id (drawn, or read from the caller's
+// negatives), bounds-checked; a drawn id is handed back when asked
+__device__ __forceinline__ int32_t slot_entity(const StepArgs& A, int64_t i, int j, int* err) {
+  int kind; uint64_t n, poff;
+  slot_layout(A.side_mode, A.Kside, i, j, &kind, &n, &poff);
+  int64_t e;
+  if (A.given) {
+    e = load_idx(A.neg_user, i * A.Keff + j, A.i64);
+  } else {
+    const int64_t x = load_idx(A.pos, i * 3 + (kind == KIND_HC ? 0 : 2), A.i64);
+    if (A.smp.kind == KGE_SAMPLER_TYPED && (x < 0 || x >= A.ent.rows)) { e = 0; *err = KGE_ERANGE; }
+    else {
+      e = sample_entity(A.smp, A.smp.offset + poff, n, x, err);   // plane offset (+1 for the t side)
+      if (e < 0) e = 0;
+    }
+    if (A.neg_user) store_idx(A.neg_user, i * A.Keff + j, e, A.i64);
+  }
+  if (e < 0 || e >= A.ent.rows) { *err = KGE_ERANGE; e = 0; }
+  return (int32_t)e;
+}
+
 // compile-time loop over u = 0 .. N-1 (fn gets std::integral_constant<int, u>)
 template <class Fn, int... Is>
 __device__ __forceinline__ void static_for_impl(Fn& fn, std::integer_sequence<int, Is...>) {
@@ -252,45 +273,31 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
   const int64_t i0 = (int64_t)blockIdx.x * nP;
   const int nValid = (int)min<int64_t>((int64_t)nP, A.B - i0);
 
-  // positive ids of the workgroup
-  if (tid < nValid * 3) {
-    const int p = tid / 3, c = tid % 3;
-    int64_t v = load_idx(A.pos, (i0 + p) * 3 + c, A.i64);
-    const int64_t lim = c == 1 ? A.rel.rows : A.ent.rows;
-    if (v < 0 || v >= lim) { err = KGE_ERANGE; v = 0; }
-    s_pos[tid] = v;
-  }
-  // negative ids (draw or read), bounds-checked
-  for (int s = tid; s < nValid * Keff; s += blockDim.x) {
-    const int p = s / Keff, j = s % Keff;
-    const int64_t i = i0 + p;
-    int kind; uint64_t n, poff;
-    slot_layout(A.side_mode, A.Kside, i, j, &kind, &n, &poff);
-    int64_t e;
-    if (A.given) {
-      e = load_idx(A.neg_user, i * Keff + j, A.i64);
-    } else {
-      const int64_t x = load_idx(A.pos, i * 3 + (kind == KIND_HC ? 0 : 2), A.i64);
-      if (A.smp.kind == KGE_SAMPLER_TYPED && (x < 0 || x >= A.ent.rows)) { e = 0; err = KGE_ERANGE; }
-      else {
-        e = sample_entity(A.smp, A.smp.offset + poff, n, x, &err);   // plane offset (+1 for the t side)
-        if (e < 0) e = 0;
-      }
-      if (A.neg_user) store_idx(A.neg_user, i * Keff + j, e, A.i64);
-    }
-    if (e < 0 || e >= A.ent.rows) { err = KGE_ERANGE; e = 0; }
-    s_ids[s] = (int32_t)e;
-  }
-  __syncthreads();
-  KGE_PROF(0);
-
   const bool active = grp < nValid;
   const int64_t i = i0 + grp;
   const int jbeg = min(Keff, gw * A.SW);
   const int jend = min(Keff, jbeg + A.SW);
-  const int32_t* ids = s_ids + grp * Keff;
+  int32_t* ids = s_ids + grp * Keff;
   float* gR = s_R + grp * Keff;
   float* gT = s_T + grp * Keff;
+
+  // every wave fetches its positive's ids and draws its own slots (no
+  // workgroup barrier: the slots' ids are read back by this wave only)
+  int64_t ph = 0, pr = 0, pt = 0;
+  if (active) {
+    ph = load_idx(A.pos, i * 3 + 0, A.i64);
+    pr = load_idx(A.pos, i * 3 + 1, A.i64);
+    pt = load_idx(A.pos, i * 3 + 2, A.i64);
+    if (ph < 0 || ph >= A.ent.rows) { err = KGE_ERANGE; ph = 0; }
+    if (pr < 0 || pr >= A.rel.rows) { err = KGE_ERANGE; pr = 0; }
+    if (pt < 0 || pt >= A.ent.rows) { err = KGE_ERANGE; pt = 0; }
+    if (gw == 0 && lane < 3) s_pos[grp * 3 + lane] = lane == 0 ? ph : lane == 1 ? pr : pt;
+    for (int j = jbeg + lane; j < jend; j += KGE_WAVE) ids[j] = slot_entity(A, i, j, &err);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  KGE_PROF(0);
 
   typename M::Ctx ctx;
   float Mrun = -INFINITY, Zs = 0.f, csum = 0.f;
@@ -299,7 +306,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
   accH.zero(); accR.zero(); accT.zero();
   float Rp = 0.f, tp = 1.f, sp = 0.f, lpp = 0.f;
   if (active) {
-    M::load_ctx(ctx, A.ent, A.rel, s_pos[grp * 3 + 0], s_pos[grp * 3 + 1], s_pos[grp * 3 + 2], mp);
+    M::load_ctx(ctx, A.ent, A.rel, ph, pr, pt, mp);
     {   // the positive's score, in every wave (hinge / logistic weights need it)
       F a, b, E0;
       E0.zero();
@@ -468,7 +475,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
     float rsq = 0.f;
     if (A.rel_reg != 0.f) {   // DistMult: lambda * mean_i ||r_i||^2 (DistMult.py:164-165)
       F Rr;
-      load_row(Rr, A.rel.row(s_pos[grp * 3 + 1]), A.rel.cols);
+      load_row(Rr, A.rel.row(pr), A.rel.cols);
       rsq = wave_sum(sq_partial(Rr));
     }
     if (lane == 0) {
