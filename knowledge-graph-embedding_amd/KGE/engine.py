@@ -66,7 +66,7 @@ def fused_plan(model, optimizer):
     return None
 
 
-FUSED_MODELS = (_hip.MODEL_TRANSE, _hip.MODEL_DISTMULT, _hip.MODEL_ROTATE)
+FUSED_MODELS = (_hip.MODEL_TRANSE, _hip.MODEL_DISTMULT, _hip.MODEL_ROTATE, _hip.MODEL_RESCAL)
 
 
 def fused_names(model):

@@ -51,6 +51,10 @@ class RESCAL(SemanticModel):
         assert list(model_weights["ent_emb"].shape) == [E, k], "shape of 'ent_emb' should be (len(metadata['ind2ent']), embedding_params['embedding_size'])"
         assert list(model_weights["rel_inter"].shape) == [R, k, k], "shape of 'rel_inter' should be (len(metadata['ind2rel']), embedding_params['embedding_size'], embedding_params['embedding_size'])"
 
+    def _fused_tables(self):
+        return {"ent": self.model_weights["ent_emb"], "rel": self.model_weights["rel_inter"],
+                "dim": self.embedding_params["embedding_size"]}
+
     def score_hrt(self, h, r, t):
         """``RESCAL.py:140-174``."""
         h, r, t = super(RESCAL, self).score_hrt(h, r, t)

@@ -45,6 +45,9 @@ struct Plan {
   uint64_t ws_bytes;
   // workspace offsets
   uint64_t o_ctl, o_cnt, o_coef, o_snap, o_gpos, o_part, o_list, o_ovf;
+  // dense-gradient / relation-matrix models (RESCAL)
+  uint64_t o_upart, o_sorted, o_srel, o_gproj, o_rpart, o_regpart, o_gent, o_grel;
+  bool rescal;
 };
 
 int score_sk(int kind, float p) {
@@ -67,14 +70,24 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   if (d->abi_version != KGE_ABI_VERSION)
     return fail(KGE_EINVAL, "abi_version %d != library %d", d->abi_version, KGE_ABI_VERSION);
   const int model = d->model;
-  if (model != KGE_MODEL_TRANSE && model != KGE_MODEL_DISTMULT && model != KGE_MODEL_ROTATE)
+  if (model != KGE_MODEL_TRANSE && model != KGE_MODEL_DISTMULT && model != KGE_MODEL_ROTATE &&
+      model != KGE_MODEL_RESCAL)
     return fail(KGE_EUNSUPPORTED, "model %d has no fused kernel in this build", model);
   if (d->dim <= 0) return fail(KGE_EINVAL, "dim must be > 0");
+  const bool rescal = model == KGE_MODEL_RESCAL;
   const int64_t entc = model == KGE_MODEL_ROTATE ? 2 * (int64_t)d->dim : d->dim;
-  const int64_t relc = d->dim;
+  const int64_t relc = rescal ? (int64_t)d->dim * d->dim : d->dim;   // RESCAL: [R, d, d] matrices
   kge_status s;
   if ((s = check_table(d->ent, "ent_emb", entc))) return s;
-  if ((s = check_table(d->rel, model == KGE_MODEL_DISTMULT ? "rel_inter" : "rel_emb", relc))) return s;
+  if ((s = check_table(d->rel, (model == KGE_MODEL_DISTMULT || rescal) ? "rel_inter" : "rel_emb", relc))) return s;
+  if (rescal) {
+    // the regulariser makes both gradients dense (RESCAL.py:190-198); without
+    // it TF clips by per-lookup slice norms, which need every negative's
+    // projection R e -- that case stays on the plugin path
+    if (!d->constraint)
+      return fail(KGE_EUNSUPPORTED, "RESCAL with constraint=False (slice-norm clipping) has no fused kernel");
+    if (d->dim > 256) return fail(KGE_EUNSUPPORTED, "RESCAL fused step supports d <= 256 (got %d)", d->dim);
+  }
   if (d->batch < 0) return fail(KGE_EINVAL, "batch must be >= 0");
   if (d->negative_ratio < 0) return fail(KGE_EINVAL, "negative_ratio must be >= 0");
   if (d->corrupt_side < KGE_SIDE_H || d->corrupt_side > KGE_SIDE_HT)
@@ -132,7 +145,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   } else {
     vec = (entc % 4 == 0 && relc % 4 == 0 && d->ent.ld % 4 == 0 && d->rel.ld % 4 == 0 && a16) ? 4 : 1;
   }
-  const int64_t rowlen = std::max(entc, relc);
+  const int64_t rowlen = rescal ? entc : std::max(entc, relc);   // fragment row length
   const int nc = (int)ceil_div(rowlen, 64 * vec);
   if (nc > 4)
     return fail(KGE_EUNSUPPORTED, "row of %lld floats exceeds the fused kernel's %d", (long long)rowlen, 256 * vec);
@@ -150,7 +163,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   if (nWG > 0x7fffffff) return fail(KGE_EUNSUPPORTED, "batch %lld too large", (long long)B);
   // destination keys: codes i*Keff + j (negatives), B*Keff + 3i + c (positive rows)
   const int64_t E = d->ent.rows, R = d->rel.rows;
-  const int64_t ndest = E + R;
+  const int64_t ndest = rescal ? E : E + R;   // RESCAL's relation gradient comes from the dR pass
   const int64_t T = B * (Keff + 3);
   // destination codes: (i << kshift) | j for slot j of positive i, then
   // (B << kshift) + 4 i + c for the positive's own rows (shift-decoded)
@@ -158,7 +171,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   while ((1LL << kshift) < Keff) ++kshift;
   if ((B << kshift) + 4 * B >= (int64_t)0xFFFFFFFF)
     return fail(KGE_EUNSUPPORTED, "batch x negative_ratio too large for 32-bit destination codes");
-  if (B * 3 * std::max(entc, relc) >= (int64_t)0xFFFFFFFF)
+  if (B * 3 * rowlen >= (int64_t)0xFFFFFFFF)
     return fail(KGE_EUNSUPPORTED, "batch x embedding size too large for 32-bit context offsets");
   // per-destination list capacity: ~4x the mean load, 64..256 entries (the
   // update kernel orders up to 256 in registers; longer lists overflow)
@@ -173,6 +186,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.G.nc = ncp;
   P.G.nWG = (int)nWG;
   P.G.gridU = (int)ceil_div(ndest, kUpdWaves);
+  P.rescal = rescal;
   P.G.lds_score = (size_t)SL.total;
   if (P.G.lds_score > 160 * 1024)
     return fail(KGE_EUNSUPPORTED, "LDS budget exceeded (score kernel %zu bytes)", P.G.lds_score);
@@ -210,6 +224,9 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.inv_bk = (float)(1.0 / (bg * Keff));
   A.limit = d->rotate_limit;
   A.rel_reg = (model == KGE_MODEL_DISTMULT && d->constraint) ? d->constraint_weight : 0.f;
+  A.rel_dests = !rescal;
+  A.dense = rescal && A.train;
+  A.dense_ent = rescal ? (float)(2.0 * d->constraint_weight / (double)E) : 0.f;
   A.lr = d->lr;
   A.clip_norm = d->clip_norm;
   A.wpp = wpp;
@@ -221,7 +238,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.nkeyneg = (uint32_t)(B << kshift);
   A.snap_cols = (int32_t)entc;
   A.gcols = (int32_t)rowlen;
-  A.rel_gcols = (int32_t)relc;
+  A.rel_gcols = (int32_t)(rescal ? entc : relc);
   A.loss_out = d->loss_out;
   A.loss_accum = d->loss_accum;
   A.pos_score_out = d->pos_score_out;
@@ -241,6 +258,19 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.o_part = take((uint64_t)nWG * 8 * 4);
   P.o_list = take((uint64_t)ndest * cap * 4);
   P.o_ovf = take((uint64_t)T * 8);
+  P.o_upart = take((uint64_t)P.G.gridU * 4);
+  if (rescal) {
+    const int64_t nct = ceil_div(d->dim, 16);
+    P.o_sorted = take((uint64_t)B * 4);
+    P.o_srel = take((uint64_t)B * 4);
+    P.o_gproj = take((uint64_t)B * 2 * entc * 4);
+    P.o_rpart = take((uint64_t)R * nct * 4);
+    P.o_regpart = take((uint64_t)kRegWGs * 2 * 4);
+    if (d->optimizer == KGE_OPT_SGD) {   // dense gradients (KGE_OPT_GRAD: the caller's grad_out)
+      P.o_gent = take((uint64_t)E * entc * 4);
+      P.o_grel = take((uint64_t)R * relc * 4);
+    }
+  }
   P.ws_bytes = std::max<uint64_t>(off, 256);
   return KGE_OK;
 }
@@ -350,10 +380,39 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   A.part = (float*)(ws + P.o_part);
   A.list = (uint32_t*)(ws + P.o_list);
   A.ovf = (uint64_t*)(ws + P.o_ovf);
+  A.upart = (float*)(ws + P.o_upart);
+  A.gpe = A.gpos;
+  A.gpe_stride = 3 * A.gcols;
+  A.gpe_toff = 2 * A.gcols;
+  RelArgs RA{};
+  if (P.rescal) {
+    A.gpe = (float*)(ws + P.o_gproj);
+    A.gpe_stride = 2 * d->dim;
+    A.gpe_toff = d->dim;
+    if (d->optimizer == KGE_OPT_SGD) A.gent = (float*)(ws + P.o_gent);
+    RA.ent = A.ent;
+    RA.rel = A.rel;
+    RA.pos = A.pos;
+    RA.i64 = A.i64;
+    RA.B = A.B;
+    RA.d = d->dim;
+    RA.sorted = (int32_t*)(ws + P.o_sorted);
+    RA.srel = (int32_t*)(ws + P.o_srel);
+    RA.snap = A.snap;
+    RA.gpos = A.gpos;
+    RA.gcols = A.gcols;
+    RA.gproj = A.gpe;
+    RA.grel = d->optimizer == KGE_OPT_SGD ? (float*)(ws + P.o_grel) : d->grad_out[1];
+    RA.rpart = (float*)(ws + P.o_rpart);
+    RA.dense_rel = (float)(2.0 * d->constraint_weight / (double)A.rel.rows);
+    RA.ctl = A.ctl;
+    RA.norm2_out = A.norm2_out;
+    RA.status = A.status;
+  }
 
   hipEvent_t const* ev = (hipEvent_t const*)d->prof_events;
   if (ev) (void)hipEventRecord(ev[0], st);
-  if (A.grad_mode) {
+  if (A.grad_mode && !P.rescal) {   // RESCAL's dense passes write every row
     (void)hipMemsetAsync(d->grad_out[0], 0, (size_t)A.ent.rows * A.ent.cols * sizeof(float), st);
     (void)hipMemsetAsync(d->grad_out[1], 0, (size_t)A.rel.rows * A.rel_gcols * sizeof(float), st);
   }
@@ -371,7 +430,25 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     return hip_check("kge_step(empty batch)");
   }
   if (ev) (void)hipEventRecord(ev[1], st);
-  s = launch_step_elementwise(A, P.G, d->model, P.sk, st, ev);
+  if (P.rescal) {
+    s = launch_step_rescal(A, P.G, RA, d->constraint ? d->constraint_weight : 0.f,
+                           (float*)(ws + P.o_regpart), st, ev);
+    if (s == KGE_OK && d->optimizer == KGE_OPT_SGD) {
+      // keras SGD on the dense gradients: clip_by_norm with the dense norm^2
+      // the update / dR passes reduced (BaseModel.py:327-328)
+      const kge_table* tabs[2] = {&d->ent, &d->rel};
+      const float* gs[2] = {A.gent, RA.grel};
+      for (int v = 0; v < 2; ++v) {
+        const kge_table& t = *tabs[v];
+        const int64_t blocks = std::min<int64_t>(ceil_div(t.rows * t.cols, 256), 8192);
+        hipLaunchKernelGGL(apply_kernel, dim3((unsigned)blocks), dim3(256), 0, st, t.data, t.rows, (int32_t)t.cols,
+                           t.ld, gs[v], (const float*)&A.ctl->dn2[v], d->lr, d->clip_norm, 0, (float*)nullptr,
+                           (float*)nullptr, 0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  } else {
+    s = launch_step_elementwise(A, P.G, d->model, P.sk, st, ev);
+  }
   if (s != KGE_OK) return fail(s, "no kernel instance for model %d / score %d", d->model, P.sk);
   if (ev) (void)hipEventRecord(ev[3], st);
   return hip_check("kge_step");

@@ -186,8 +186,9 @@ struct TabView {
 
 // Model scalars shared by every policy call.
 struct MP {
-  float limit;   // RotatE phase range (RotatE.py:93)
-  bool norm;     // fused full-table renormalisation: h / t context rows normalised on load
+  float limit;       // RotatE phase range (RotatE.py:93)
+  bool norm;         // fused full-table renormalisation: h / t context rows normalised on load
+  const float* ctx;  // RESCAL: this positive's precomputed context rows (u = R^T h, v = R t)
 };
 
 // Context rows ("snap") written per positive by the score kernel and read
@@ -546,6 +547,81 @@ struct RotatE {
         gE.v[i + 1] = g.v[i + 1] * co - g.v[i] * si;
       }
     }
+  }
+};
+
+// ======================================================================
+// RESCAL: h^T R_r t     (RESCAL.py:140-174); score_fn not used
+// The relation matrix never enters the score kernel: a separate MFMA pass
+// (kge_rel.hip) writes each positive's context rows u = R^T h (snap row 0)
+// and v = R t (snap row 1) first, so every triple of the positive is a dot
+// product of two d-vectors:
+//   positive      u . t
+//   t-corrupted   u . e          (gradient wrt e: alpha u)
+//   h-corrupted   e . v          (gradient wrt e: alpha v)
+// The positive's own rows need R again: g_h = R (c_p t + sum_tc alpha e),
+// g_t = R^T (c_p h + sum_hc alpha e). The score kernel therefore leaves the
+// UN-projected sums in the positive-gradient rows -- row 0: A = c_p t +
+// sum_tc alpha e, row 1: b = sum_hc alpha e, row 2: B = c_p h + b -- and the
+// MFMA pass after it projects them and forms dR_r = sum_i h_i (x) A_i + b_i (x) t_i.
+// ======================================================================
+template <int VEC, int NC, int SK_UNUSED>
+struct Rescal {
+  static constexpr bool CPLX = false;
+  static constexpr int NSNAP = 2;
+  using F = Frag<VEC, NC>;
+  struct Ctx { F H, T, U, V; };
+  struct ECtx { F c0; };
+
+  __device__ static void load_ctx(Ctx& c, const TabView& ent, const TabView&, int64_t h, int64_t,
+                                  int64_t t, const MP& mp) {
+    load_row(c.H, ent.row(h), ent.cols);
+    load_row(c.T, ent.row(t), ent.cols);
+    load_row(c.U, mp.ctx, ent.cols);
+    load_row(c.V, mp.ctx + ent.cols, ent.cols);
+  }
+  __device__ static void fwd(const Ctx& c, int kind, const F& E, F& a, F& b) {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) {
+      a.v[i] = kind == KIND_HC ? E.v[i] : c.U.v[i];
+      b.v[i] = kind == KIND_HC ? c.V.v[i] : (kind == KIND_TC ? E.v[i] : c.T.v[i]);
+    }
+  }
+  // POS (called at unit alpha): row 0 gets t, row 2 gets h (scaled by c_p
+  // in the merge); TC: row 0 += alpha e; HC: rows 1 and 2 += alpha e
+  __device__ static void bwd(const Ctx& c, int kind, const F& E, const F&, const F&, float alpha, float,
+                             F& accH, F& accR, F& accT, float*, const MP&) {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) {
+      if (kind == KIND_POS) {
+        accH.v[i] += alpha * c.T.v[i];
+        accT.v[i] += alpha * c.H.v[i];
+      } else if (kind == KIND_TC) {
+        accH.v[i] += alpha * E.v[i];
+      } else {
+        accR.v[i] += alpha * E.v[i];
+        accT.v[i] += alpha * E.v[i];
+      }
+    }
+  }
+  static constexpr bool NRM_FROM_R = false;
+  static constexpr bool LINEAR_E = true;   // gradient wrt a sampled entity row: alpha * (u or v)
+  __device__ static void lin_coefs(int, float alpha, float& aE, float& aC) { aE = 0.f; aC = alpha; }
+  template <int KIND>
+  __device__ static void fwdk(const Ctx& c, const F& E, F& a, F& b) { fwd(c, KIND, E, a, b); }
+  template <int KIND>
+  __device__ static void bwdk(const Ctx& c, const F& E, const F& a, const F& b, float alpha, float M,
+                              F& accH, F& accR, F& accT, float* nrm, const MP& mp) {
+    bwd(c, KIND, E, a, b, alpha, M, accH, accR, accT, nrm, mp);
+  }
+  __device__ static void finish(F&, F&, F&) {}
+  __device__ static void write_snap(const Ctx&, float*, int) {}   // written by the context pass
+  __device__ static void load_ectx(const float* sb, int cols, int kind, ECtx& ec) {
+    load_row(ec.c0, sb + (kind == KIND_TC ? 0 : cols), cols);
+  }
+  __device__ static void grad_entity(const ECtx& ec, int, const F&, float alpha, float, F& gE) {
+#pragma unroll
+    for (int i = 0; i < VEC * NC; ++i) gE.v[i] = alpha * ec.c0.v[i];
   }
 };
 

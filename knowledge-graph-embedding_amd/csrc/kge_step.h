@@ -19,10 +19,13 @@ struct StepCtl {
   uint32_t score_ticket;   // score workgroups done (the last one reduces the partials)
   uint32_t ovf_count;      // overflow-list appends of the running score kernel
   uint32_t ovf_len;        // overflow-list length for the update kernel (set by the last score workgroup)
-  uint32_t pad0;
+  uint32_t upd_ticket;     // dense-gradient update workgroups done (entity norm^2)
   float scale[4];          // -lr * clip / max(||g_v||, clip) per variable
   float loss;
-  float pad1[7];
+  uint32_t rel_ticket;     // relation-matrix gradient workgroups done (rel norm^2)
+  uint32_t reg_ticket;     // regulariser-loss workgroups done
+  uint32_t pad0;
+  float dn2[4];            // norm^2 of the dense (duplicate-summed) gradient per variable
 };
 
 // Everything a step kernel needs, passed by value (kernarg segment).
@@ -49,6 +52,17 @@ struct StepArgs {
   float limit;
   float rel_reg;    // DistMult constraint_weight (0 = off): lambda * mean_i ||r_i||^2
   float lr, clip_norm;
+  // dense-gradient variables (a full-table regulariser term makes TF's
+  // gradient dense: RESCAL.py:190-198): the update kernel visits every row,
+  // adds dense_ent * row, writes the summed gradient to gent and reduces its
+  // norm^2 (clip_by_norm of the dense tensor); the apply pass follows
+  bool dense;
+  bool rel_dests;   // relation rows are update-kernel destinations (false: RESCAL's dR pass)
+  float dense_ent;  // d(regulariser)/d(row) coefficient of every entity row
+  // positives' own entity-row gradients: row h at gpe + i*gpe_stride, t at + gpe_toff
+  float* gpe;
+  int32_t gpe_stride, gpe_toff;
+  float* upart;     // [gridU] update-kernel norm^2 partials (dense mode)
   // geometry
   int32_t wpp;      // waves per positive (1, 2, 4, 8)
   int32_t nP;       // positives per score workgroup = kStepWaves / wpp
@@ -87,6 +101,40 @@ struct StepGeom {
 
 kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int model, int sk,
                                    hipStream_t st, hipEvent_t const* ev);
+// per-family instances (kge_step_<family>.hip)
+kge_status launch_transe(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st, hipEvent_t const* ev);
+kge_status launch_distmult(const StepArgs& A, const StepGeom& G, hipStream_t st, hipEvent_t const* ev);
+kge_status launch_rotate(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st, hipEvent_t const* ev);
+
+// ---- relation-matrix models (kge_rel.hip): RESCAL's MFMA passes
+struct RelArgs {
+  TabView ent, rel;          // rel rows are d x d matrices (ld >= d*d)
+  const void* pos;
+  bool i64;
+  int64_t B;
+  int32_t d;
+  int32_t* sorted;           // [B] positives in relation order (stable)
+  int32_t* srel;             // [B] relation of sorted position p
+  float* snap;               // [B, 2, d] u = R^T h, v = R t
+  const float* gpos;         // [B, 3, gcols] A, b, B (score kernel)
+  int32_t gcols;
+  float* gproj;              // [B, 2, d] g_h = R A, g_t = R^T B
+  float* grel;               // [R, d*d] dense relation gradient
+  float* rpart;              // [R * ceil(d/16)] norm^2 partials
+  float dense_rel;           // 2 lambda / R (0: no regulariser)
+  StepCtl* ctl;
+  float* norm2_out;
+  int32_t* status;
+};
+void launch_rel_rank(const RelArgs& R, hipStream_t st);
+void launch_rel_ctx(const RelArgs& R, hipStream_t st);      // u, v
+void launch_rel_post(const RelArgs& R, hipStream_t st);     // g_h, g_t, dR (+ dense term, norm^2)
+// lambda * (mean_e ||e||^2 + mean_r ||R_r||_F^2) added to the step loss (RESCAL.py:190-198)
+void launch_reg_loss(const TabView& ent, const TabView& rel, float lam, float* part, StepCtl* ctl,
+                     float* loss_out, float* loss_accum, hipStream_t st);
+constexpr int kRegWGs = 256;
+kge_status launch_step_rescal(const StepArgs& A, const StepGeom& G, const RelArgs& P, float lam, float* regpart,
+                              hipStream_t st, hipEvent_t const* ev);
 
 __global__ void constrain_rows_kernel(float* t, int64_t rows, int32_t cols, int64_t ld, int kind,
                                       float value);

@@ -1,0 +1,980 @@
+// Fused KGE training step for gfx950 -- kernel templates (score / update).
+// Instantiated per model family in kge_step_<family>.hip (parallel builds);
+// kge_step.hip holds the non-template kernels and the dispatch.
+//
+// One reference batch step (KGEModel.__run_single_batch, BaseModel.py:293-330)
+// runs as stream-ordered kernels:
+//
+//   K0  constrain   full-table row renormalisation of ent_emb when the model's
+//                   _constraint_loss assigns it (TransE.py:171-172,
+//                   DistMult.py:162-163).
+//   KS  score       8-wave workgroups, `wpp` waves per positive. In-register
+//                   Philox negative draws (ns_strategy.py:39-64 in the layout
+//                   of BaseModel.py:332-408); each wave streams its slots'
+//                   rows in register batches (gather -> forward -> ONE
+//                   transposed multi-reduction per batch -> loss weight ->
+//                   backward), with SANS's softmax folded in online (loss.py
+//                   :174-182), so every sampled row is read exactly once. The
+//                   positive's own rows are reduced on chip; every negative
+//                   leaves one (alpha, value) coefficient and its destination
+//                   key, filed straight into that destination's list (one
+//                   int atomic per key). The last workgroup reduces the
+//                   loss and the per-variable gradient norms (clip_by_norm,
+//                   BaseModel.py:327) in a fixed order.
+//   KU  update      destination-major, one wave per entity / relation row:
+//                   its keys in ascending code order (bit-reproducible sums,
+//                   no float atomics), each negative's row gradient re-derived
+//                   from ONE frozen context row + its coefficient, the
+//                   positives' own row gradients added, clip scale and SGD
+//                   (BaseModel.py:328, keras SGD ResourceScatterAdd) applied
+//                   with ONE read-modify-write per touched row.
+#pragma once
+#include <utility>
+
+#include "kge_step.h"
+
+#ifndef KGE_STREAM_ROWS
+#define KGE_STREAM_ROWS 8   // sampled rows per stream batch at NC = 1 (tuning knob)
+#endif
+#ifndef KGE_UPDATE_U
+#define KGE_UPDATE_U 8      // update kernel: list entries in flight per wave at NC = 1 (tuning knob)
+#endif
+
+namespace kge {
+
+#ifdef KGE_PHASE_PROF
+extern __device__ unsigned long long g_kge_prof[64];
+#endif
+
+// ------------------------------------------------------------ helpers
+__device__ __forceinline__ float log_sigmoid(float x) {
+  return fminf(x, 0.f) - log1pf(expf(-fabsf(x)));
+}
+__device__ __forceinline__ float sigmoid(float x) { return 1.f / (1.f + expf(-x)); }
+
+// slot j of positive i -> corruption kind (BaseModel.py:353-356: 'h+t' rows
+// alternate [h-corrupt j/2, t-corrupt j/2]), draw index within its side's
+// counter plane, plane offset (0 = h side / single side, 1 = t side)
+__device__ __forceinline__ void slot_layout(int side_mode, int Kside, int64_t i, int j, int* kind,
+                                            uint64_t* n, uint64_t* plane_off) {
+  if (side_mode == KGE_SIDE_HT) {
+    *kind = (j & 1) ? KIND_TC : KIND_HC;
+    *n = (uint64_t)(i * Kside + (j >> 1));
+    *plane_off = (j & 1);
+  } else {
+    *kind = side_mode == KGE_SIDE_H ? KIND_HC : KIND_TC;
+    *n = (uint64_t)(i * Kside + j);
+    *plane_off = 0;
+  }
+}
+__device__ __forceinline__ int slot_kind(int side_mode, int j) {
+  if (side_mode == KGE_SIDE_HT) return (j & 1) ? KIND_TC : KIND_HC;
+  return side_mode == KGE_SIDE_H ? KIND_HC : KIND_TC;
+}
+
+__device__ __forceinline__ float bcast(float v, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
+
+// relation-row fragments: full layout, or RotatE's half layout
+template <bool HALF, int VEC>
+struct RelV { static constexpr int n = HALF ? (VEC / 2 > 0 ? VEC / 2 : 1) : VEC; };
+
+template <bool HALF, int VEC, int NC>
+__device__ __forceinline__ void load_rel_row(float (&v)[(HALF ? (VEC / 2 > 0 ? VEC / 2 : 1) : VEC) * NC], const float* row, int cols) {
+  if constexpr (HALF) {
+    load_row_half<VEC, NC>(v, row, cols);
+  } else {
+    Frag<VEC, NC> f;
+    load_row(f, row, cols);
+#pragma unroll
+    for (int q = 0; q < VEC * NC; ++q) v[q] = f.v[q];
+  }
+}
+template <bool HALF, int VEC, int NC>
+__device__ __forceinline__ void store_rel_row(const float (&v)[(HALF ? (VEC / 2 > 0 ? VEC / 2 : 1) : VEC) * NC], float* row, int cols) {
+  if constexpr (HALF) {
+    store_row_half<VEC, NC>(v, row, cols);
+  } else {
+    Frag<VEC, NC> f;
+#pragma unroll
+    for (int q = 0; q < VEC * NC; ++q) f.v[q] = v[q];
+    store_row(f, row, cols);
+  }
+}
+
+// dL/ds of one negative (loss.py); SANS with its positive's final softmax
+// reference max Ms and 1/Z
+__device__ __forceinline__ float neg_coef(const StepArgs& A, float s, float sp, float Ms, float invZ) {
+  switch (A.loss_kind) {
+    case KGE_LOSS_HINGE: return (A.margin + s - sp >= 0.f) ? A.inv_bk : 0.f;
+    case KGE_LOSS_LOGISTIC: { const float ex = expf(s - sp); return ex / (1.f + ex); }
+    case KGE_LOSS_BCE: return sigmoid(s) * A.inv_b;
+    case KGE_LOSS_SANS: return expf(A.temperature * s - Ms) * invZ * sigmoid(s + A.margin) * A.inv_b;
+    default: return s * A.inv_b;
+  }
+}
+
+// one destination key: append its code to the destination's list (arrival
+// order), or to the overflow list once that list is full
+__device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_t code) {
+  const uint32_t r = atomicAdd(&A.cnt[dest], 1u);
+  if (r < (uint32_t)A.cap) {
+    A.list[dest * A.cap + r] = code;
+  } else {
+    const uint32_t o = atomicAdd(&A.ctl->ovf_count, 1u);
+    A.ovf[o] = ((uint64_t)dest << 32) | code;
+  }
+}
+
+// slot j of positive i: its entity id (drawn, or read from the caller's
+// negatives), bounds-checked; a drawn id is handed back when asked
+__device__ __forceinline__ int32_t slot_entity(const StepArgs& A, int64_t i, int j, int* err) {
+  int kind; uint64_t n, poff;
+  slot_layout(A.side_mode, A.Kside, i, j, &kind, &n, &poff);
+  int64_t e;
+  if (A.given) {
+    e = load_idx(A.neg_user, i * A.Keff + j, A.i64);
+  } else {
+    const int64_t x = load_idx(A.pos, i * 3 + (kind == KIND_HC ? 0 : 2), A.i64);
+    if (A.smp.kind == KGE_SAMPLER_TYPED && (x < 0 || x >= A.ent.rows)) { e = 0; *err = KGE_ERANGE; }
+    else {
+      e = sample_entity(A.smp, A.smp.offset + poff, n, x, err);   // plane offset (+1 for the t side)
+      if (e < 0) e = 0;
+    }
+    if (A.neg_user) store_idx(A.neg_user, i * A.Keff + j, e, A.i64);
+  }
+  if (e < 0 || e >= A.ent.rows) { *err = KGE_ERANGE; e = 0; }
+  return (int32_t)e;
+}
+
+// compile-time loop over u = 0 .. N-1 (fn gets std::integral_constant<int, u>)
+template <class Fn, int... Is>
+__device__ __forceinline__ void static_for_impl(Fn& fn, std::integer_sequence<int, Is...>) {
+  (fn(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, class Fn>
+__device__ __forceinline__ void static_for(Fn&& fn) {
+  static_for_impl(fn, std::make_integer_sequence<int, N>{});
+}
+
+// corruption kind of row u of a stream batch (batches start on an even slot:
+// 'h+t' slots alternate h-corrupt / t-corrupt, BaseModel.py:353-356)
+template <int SIDE>
+__host__ __device__ constexpr int kind_at(int u) {
+  return SIDE == KGE_SIDE_HT ? ((u & 1) ? KIND_TC : KIND_HC) : SIDE == KGE_SIDE_H ? KIND_HC : KIND_TC;
+}
+
+// per-positive merge slots (LDS)
+enum { MG_F = 0, MG_AP = 8, MG_LOSS = 9, MG_N = 10, MG_UN = 16, MG_RP = 20, MG_TP = 21, MG_SP = 22, MG_LPP = 23,
+       MG_RSQ = 24, MG_MS = 25, MG_IZ = 26, MG_STRIDE = kMergeStride };
+static_assert(MG_IZ < MG_STRIDE, "merge slots exceed the LDS stride");
+
+// ------------------------------------------------------------ KS score
+// One workgroup = kStepWaves waves = nP positives x wpp waves. A wave owns
+// SW consecutive negative slots of its positive and streams them in batches
+// of ROWS rows held in registers: gather (one global_load_dwordx4 per row
+// per lane), forward, ONE transposed multi-reduction for the whole batch,
+// per-row loss weight computed by the lanes that hold that row's score,
+// analytic backward into the positive's h / r / t accumulators. SANS's
+// softmax is folded in online (running max; accumulators rescaled when it
+// grows), so no row outlives its batch and no row is read twice. The
+// positive's waves merge their states through LDS; then every wave
+// finalises its slots' coefficients and files every destination key into
+// that destination's list for the update kernel.
+template <template <int, int, int> class Model, int VEC, int NC, int SK, int SIDE>
+__global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4))) void score_kernel(StepArgs A) {
+  using M = Model<VEC, NC, SK>;
+  using F = Frag<VEC, NC>;
+  constexpr int W = kStepWaves;
+  constexpr int FL = KGE_WAVE * VEC * NC;   // floats per fragment image
+  constexpr int ROWS = KGE_STREAM_ROWS / NC > 1 ? KGE_STREAM_ROWS / NC : 2;   // rows per batch (in registers)
+  constexpr int SH = ROWS == 16 ? 2 : ROWS == 8 ? 3 : ROWS == 4 ? 4 : 5;   // lane l holds row l >> SH after multi_reduce
+  constexpr int LPR = 1 << SH;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int Keff = A.Keff, nP = A.nP, wpp = A.wpp;
+  const ScoreLds L = score_lds(FL, nP, Keff);
+  int64_t* s_pos = reinterpret_cast<int64_t*>(smem + L.pos);
+  int32_t* s_ids = reinterpret_cast<int32_t*>(smem + L.ids);
+  float* s_R = reinterpret_cast<float*>(smem + L.sR);
+  float* s_T = reinterpret_cast<float*>(smem + L.sT);
+  float* s_st = reinterpret_cast<float*>(smem + L.st);
+  float* s_mrg = reinterpret_cast<float*>(smem + L.mrg);
+  float* red = reinterpret_cast<float*>(smem + L.red);
+  float* posg = reinterpret_cast<float*>(smem + L.posg);
+  float* s_misc = reinterpret_cast<float*>(smem + L.misc);
+  __shared__ int s_last;
+
+  KGE_PROF_INIT();
+  const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const int grp = wv / wpp, gw = wv % wpp;
+  int err = 0;
+
+  const int64_t i0 = (int64_t)blockIdx.x * nP;
+  const int nValid = (int)min<int64_t>((int64_t)nP, A.B - i0);
+
+  const bool active = grp < nValid;
+  const int64_t i = i0 + grp;
+  const MP mp{A.limit, A.fuse_norm, A.snap + (active ? i : 0) * (M::NSNAP * (int64_t)A.snap_cols)};
+  const int jbeg = min(Keff, gw * A.SW);
+  const int jend = min(Keff, jbeg + A.SW);
+  int32_t* ids = s_ids + grp * Keff;
+  float* gR = s_R + grp * Keff;
+  float* gT = s_T + grp * Keff;
+
+  // every wave fetches its positive's ids and draws its own slots (no
+  // workgroup barrier: the slots' ids are read back by this wave only)
+  int64_t ph = 0, pr = 0, pt = 0;
+  if (active) {
+    ph = load_idx(A.pos, i * 3 + 0, A.i64);
+    pr = load_idx(A.pos, i * 3 + 1, A.i64);
+    pt = load_idx(A.pos, i * 3 + 2, A.i64);
+    if (ph < 0 || ph >= A.ent.rows) { err = KGE_ERANGE; ph = 0; }
+    if (pr < 0 || pr >= A.rel.rows) { err = KGE_ERANGE; pr = 0; }
+    if (pt < 0 || pt >= A.ent.rows) { err = KGE_ERANGE; pt = 0; }
+    if (gw == 0 && lane < 3) s_pos[grp * 3 + lane] = lane == 0 ? ph : lane == 1 ? pr : pt;
+    for (int j = jbeg + lane; j < jend; j += KGE_WAVE) ids[j] = slot_entity(A, i, j, &err);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  KGE_PROF(0);
+
+  typename M::Ctx ctx;
+  float Mrun = -INFINITY, Zs = 0.f, csum = 0.f;
+  float nrm[4] = {0.f, 0.f, 0.f, 0.f};
+  F accH, accR, accT;
+  accH.zero(); accR.zero(); accT.zero();
+  float Rp = 0.f, tp = 1.f, sp = 0.f, lpp = 0.f;
+  if (active) {
+    M::load_ctx(ctx, A.ent, A.rel, ph, pr, pt, mp);
+    {   // the positive's score, in every wave (hinge / logistic weights need it)
+      F a, b, E0;
+      E0.zero();
+      M::fwd(ctx, KIND_POS, E0, a, b);
+      const float part = score_partial<SK, M::CPLX>(a, b);
+      Rp = lane_reduce<5, SK == SK_PINF>(part);
+      if (SK == SK_PINF) tp = lane_reduce<5, false>(tie_partial<M::CPLX>(a, Rp));
+      sp = score_value<SK>(Rp, A.pw, &lpp);
+    }
+    const int lrow = lane >> SH;
+    const bool lead = (lane & (LPR - 1)) == 0;
+    // RAW: unmasked row loads, only the score partial masked (NRM_FROM_R
+    // models keep no per-element norm, single-chunk rows)
+    constexpr bool RAW = M::NRM_FROM_R && NC == 1;
+    const bool lane_in = lane * VEC < A.ent.cols;
+    int idv = 0;   // the wave's next 64 slot ids, one per lane
+    for (int j0 = jbeg; j0 < jend; j0 += ROWS) {
+      if (((j0 - jbeg) & (KGE_WAVE - 1)) == 0) idv = (j0 + lane < jend) ? ids[j0 + lane] : 0;
+      const int jo = (j0 - jbeg) & (KGE_WAVE - 1);
+      const int nrow = min(ROWS, jend - j0);   // wave-uniform, >= 1
+      // every row's load is issued before any is used; rows past the slot
+      // range repeat the last valid row (finite values, weight 0)
+      // (NRM_FROM_R models: lanes past the row's end keep whatever they
+      // loaded and only their score partial is masked -- their accumulator
+      // lanes are never read back)
+      F E[ROWS];
+#pragma unroll
+      for (int u = 0; u < ROWS; ++u) {
+        const float* row = A.ent.row(__builtin_amdgcn_readlane(idv, jo + min(u, nrow - 1)));
+        if (RAW) load_row_raw(E[u], row, A.ent.cols);
+        else load_row(E[u], row, A.ent.cols);
+      }
+      if (A.fuse_norm) {
+        // fused _constraint_loss: each sampled row normalised in registers
+        // (one transposed reduction for the batch; same tree as lane_reduce)
+        float sq[ROWS];
+#pragma unroll
+        for (int u = 0; u < ROWS; ++u) sq[u] = (!RAW || lane_in) ? norm_partial(E[u]) : 0.f;
+        const float inv = inv_norm(multi_reduce<ROWS, false>(sq));
+#pragma unroll
+        for (int u = 0; u < ROWS; ++u) scale_row(E[u], bcast(inv, u << SH));
+      }
+      F a[ROWS], b[ROWS];
+      float part[ROWS];
+      static_for<ROWS>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        M::template fwdk<kind_at<SIDE>(u)>(ctx, E[u], a[u], b[u]);
+        part[u] = (u < nrow && (!RAW || lane_in)) ? score_partial<SK, M::CPLX>(a[u], b[u]) : 0.f;
+      });
+      const float Rl = multi_reduce<ROWS, SK == SK_PINF>(part);
+      float tl = 1.f;
+      if constexpr (SK == SK_PINF) {
+        float tq[ROWS];
+#pragma unroll
+        for (int u = 0; u < ROWS; ++u) tq[u] = u < nrow ? tie_partial<M::CPLX>(a[u], bcast(Rl, u << SH)) : 0.f;
+        tl = multi_reduce<ROWS, false>(tq);
+      }
+      const int j = j0 + lrow;
+      const bool valid = lrow < nrow;
+      // this lane's row weight dL/ds (loss.py; the loss VALUE is summed in
+      // the finalise pass), hardware-rate transcendentals
+      float lp;
+      const float s = score_value_fast<SK>(Rl, A.pw, &lp);
+      float c = 0.f;
+      switch (A.loss_kind) {
+        case KGE_LOSS_HINGE:
+          c = (A.margin + s - sp >= 0.f) ? A.inv_bk : 0.f;
+          if (valid && lead) csum += c;
+          break;
+        case KGE_LOSS_LOGISTIC: {
+          const float ex = fast_exp(s - sp);
+          c = ex * __builtin_amdgcn_rcpf(1.f + ex);
+          if (valid && lead) csum += c;
+        } break;
+        case KGE_LOSS_BCE:
+          c = fast_sigmoid(s) * A.inv_b;
+          break;
+        case KGE_LOSS_SANS: {
+          const float z = valid ? A.temperature * s : -INFINITY;
+          const float Mn = fmaxf(Mrun, lane_reduce<5, true>(z));
+          if (Mn > Mrun) {   // wave-uniform: rescale everything accumulated so far
+            const float sc = (Mrun == -INFINITY) ? 0.f : fast_exp(Mrun - Mn);
+            const float sc2 = sc * sc;
+#pragma unroll
+            for (int q = 0; q < VEC * NC; ++q) { accH.v[q] *= sc; accR.v[q] *= sc; accT.v[q] *= sc; }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) nrm[v] *= sc2;
+            Zs *= sc;
+            Mrun = Mn;
+          }
+          const float e = valid ? fast_exp(z - Mrun) : 0.f;
+          c = e * fast_sigmoid(s + A.margin) * A.inv_b;
+          if (valid && lead) Zs += e;
+        } break;
+        default:  // SQERR
+          c = s * A.inv_b;
+          break;
+      }
+      const float al = valid ? score_alpha_fast<SK>(c, Rl, lp, tl, A.pw) : 0.f;
+      if (valid && lead) {
+        gR[j] = Rl;
+        gT[j] = tl;
+        if (M::NRM_FROM_R) {   // ||alpha a||^2 = alpha^2 R: h- and t-lookup slices, r-lookup slice
+          const float n2 = al * al * Rl;
+          nrm[0] += 2.f * n2;
+          nrm[1] += n2;
+        }
+      }
+      // backward: rows past the range carry alpha = 0
+      static_for<ROWS>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        const float alu = bcast(al, u << SH);
+        const float Mu = SK == SK_PINF ? bcast(Rl, u << SH) : 0.f;
+        M::template bwdk<kind_at<SIDE>(u)>(ctx, E[u], a[u], b[u], alu, Mu, accH, accR, accT, nrm, mp);
+      });
+    }
+    M::finish(accH, accR, accT);
+  }
+  KGE_PROF(1);
+
+  // ---- wave state -> LDS
+  {
+    const float Zw = wave_sum(Zs), cw = wave_sum(csum);
+    float nw[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) nw[v] = wave_sum(nrm[v]);
+    if (lane == 0) {
+      float* st = s_st + wv * 8;
+      st[0] = Mrun; st[1] = Zw; st[2] = 0.f; st[3] = cw;
+      st[4] = nw[0]; st[5] = nw[1]; st[6] = nw[2]; st[7] = nw[3];
+    }
+    if (A.train) {
+      float* my = red + wv * 3 * FL;
+#pragma unroll
+      for (int q = 0; q < VEC * NC; ++q) {
+        const int c = q / VEC, k = q % VEC;
+        const int e = (c * KGE_WAVE + lane) * VEC + k;
+        my[e] = accH.v[q];
+        my[FL + e] = accR.v[q];
+        my[2 * FL + e] = accT.v[q];
+      }
+    }
+  }
+  // the positive's own gradient at unit alpha (wave 0 of each positive)
+  if (active && gw == 0) {
+    float* mg = s_mrg + grp * MG_STRIDE;
+    float pn[4] = {0.f, 0.f, 0.f, 0.f};
+    if (A.train) {
+      F pH, pR, pT, a, b, E0;
+      pH.zero(); pR.zero(); pT.zero(); E0.zero();
+      M::fwd(ctx, KIND_POS, E0, a, b);
+      M::bwd(ctx, KIND_POS, E0, a, b, 1.f, Rp, pH, pR, pT, pn, mp);
+      float* pg = posg + grp * 3 * FL;
+#pragma unroll
+      for (int q = 0; q < VEC * NC; ++q) {
+        const int c = q / VEC, k = q % VEC;
+        const int e = (c * KGE_WAVE + lane) * VEC + k;
+        pg[e] = pH.v[q];
+        pg[FL + e] = pR.v[q];
+        pg[2 * FL + e] = pT.v[q];
+      }
+      M::write_snap(ctx, A.snap + i * (M::NSNAP * (int64_t)A.snap_cols), A.snap_cols);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) pn[v] = wave_sum(pn[v]);
+    float rsq = 0.f;
+    if (A.rel_reg != 0.f) {   // DistMult: lambda * mean_i ||r_i||^2 (DistMult.py:164-165)
+      F Rr;
+      load_row(Rr, A.rel.row(pr), A.rel.cols);
+      rsq = wave_sum(sq_partial(Rr));
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) mg[MG_UN + v] = pn[v];
+      mg[MG_RP] = Rp; mg[MG_TP] = tp; mg[MG_SP] = sp; mg[MG_LPP] = lpp; mg[MG_RSQ] = rsq;
+    }
+  }
+  __syncthreads();
+  KGE_PROF(2);
+
+  // ---- merge the positive's waves (one thread per positive)
+  if (tid < nValid) {
+    const int p = tid;
+    float* mg = s_mrg + p * MG_STRIDE;
+    const float* st = s_st + p * wpp * 8;
+    const bool sans = A.loss_kind == KGE_LOSS_SANS;
+    float Ms = -INFINITY;
+    for (int g = 0; g < wpp; ++g) Ms = fmaxf(Ms, st[g * 8]);
+    float f[kMaxWpp];
+    float Z = 0.f, cw = 0.f;
+    for (int g = 0; g < wpp; ++g) {
+      const float sc = !sans ? 1.f : (st[g * 8] == -INFINITY ? 0.f : expf(st[g * 8] - Ms));
+      f[g] = sc;
+      Z += st[g * 8 + 1] * sc;
+      cw += st[g * 8 + 3];
+    }
+    const float invZ = sans ? (Z > 0.f ? 1.f / Z : 0.f) : 1.f;
+    // the positive's own loss terms; the negatives' sums come from the finalise pass
+    const float lw = 0.f;
+    const float Rpv = mg[MG_RP], tpv = mg[MG_TP], spv = mg[MG_SP], lppv = mg[MG_LPP];
+    float lossp, cp;
+    switch (A.loss_kind) {
+      case KGE_LOSS_HINGE:
+        lossp = lw * A.inv_bk;
+        cp = -cw;
+        if (Keff == 0) lossp = NAN;   // sum([]) / 0 (loss.py:81-82)
+        break;
+      case KGE_LOSS_LOGISTIC: lossp = lw; cp = -cw; break;
+      case KGE_LOSS_BCE:
+        lossp = -(log_sigmoid(spv) + lw) * A.inv_b;
+        cp = -sigmoid(-spv) * A.inv_b;
+        break;
+      case KGE_LOSS_SANS:
+        lossp = -(log_sigmoid(spv + A.margin) + lw) * A.inv_b;
+        cp = -sigmoid(-(spv + A.margin)) * A.inv_b;
+        break;
+      default:
+        lossp = ((spv - 1.f) * (spv - 1.f) + lw) * 0.5f * A.inv_b;
+        cp = (spv - 1.f) * A.inv_b;
+        break;
+    }
+    const float ap = score_alpha<SK>(cp, Rpv, lppv, tpv, A.pw);
+    float n[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) n[v] = ap * ap * mg[MG_UN + v];
+    for (int g = 0; g < wpp; ++g) {
+      const float fg = f[g] * invZ;
+      mg[MG_F + g] = fg;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) n[v] += fg * fg * st[g * 8 + 4 + v];
+    }
+    if (A.rel_reg != 0.f) {
+      // its own IndexedSlices block: (lambda / B) * 2 r  (pow-2 gradient)
+      const float gsc = A.rel_reg * A.inv_b;
+      lossp += mg[MG_RSQ] * gsc;
+      n[1] += 4.f * gsc * gsc * mg[MG_RSQ];
+    }
+    mg[MG_AP] = ap;
+    mg[MG_LOSS] = lossp;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) mg[MG_N + v] = n[v];
+    mg[MG_MS] = Ms;
+    mg[MG_IZ] = invZ;
+    if (A.pos_score_out) A.pos_score_out[i0 + p] = spv;
+  }
+  __syncthreads();
+  KGE_PROF(3);
+
+  // ---- the positives' row gradients: sum of the waves' scaled accumulators
+  if (A.train) {
+    for (int e = tid; e < nValid * 3 * FL; e += blockDim.x) {
+      const int p = e / (3 * FL), rem = e % (3 * FL);
+      const int v = rem / FL, k = rem % FL;
+      const int cols = v == 1 ? A.rel_gcols : A.ent.cols;
+      if (k >= cols) continue;
+      // RotatE keeps the phase gradient of complex element k in float 2k
+      const int src = (v == 1 && A.rel_half) ? 2 * k : k;
+      const float* mg = s_mrg + p * MG_STRIDE;
+      float s = mg[MG_AP] * posg[(p * 3 + v) * FL + src];
+      for (int g = 0; g < wpp; ++g) s += mg[MG_F + g] * red[((p * wpp + g) * 3 + v) * FL + src];
+      if (v == 1 && A.rel_reg != 0.f) s += (A.rel_reg * A.inv_b) * (2.f * A.rel.row(s_pos[p * 3 + 1])[k]);
+      A.gpos[(i0 + p) * 3 * (int64_t)A.gcols + v * (int64_t)A.gcols + k] = s;
+    }
+  }
+
+  // ---- each wave finalises its slots: loss terms, coefficient, score,
+  // destination key (one lane per slot, IEEE transcendentals)
+  float lfin = 0.f;
+  if (active) {
+    const float* mg = s_mrg + grp * MG_STRIDE;
+    const float Ms = mg[MG_MS], invZ = mg[MG_IZ], spv = mg[MG_SP];
+    for (int j = jbeg + lane; j < jend; j += KGE_WAVE) {
+      const float R = gR[j];
+      float lp;
+      const float s = score_value<SK>(R, A.pw, &lp);
+      const int64_t q = i * Keff + j;
+      switch (A.loss_kind) {
+        case KGE_LOSS_HINGE: lfin += fmaxf(A.margin + s - spv, 0.f); break;
+        case KGE_LOSS_LOGISTIC: lfin += logf(1.f + expf(s - spv)); break;
+        case KGE_LOSS_BCE: lfin += log_sigmoid(-s); break;
+        case KGE_LOSS_SANS: lfin += expf(A.temperature * s - Ms) * invZ * log_sigmoid(-s - A.margin); break;
+        default: lfin += s * s; break;
+      }
+      if (A.neg_score_out) A.neg_score_out[q] = s;
+      if (A.train) {
+        const float c = neg_coef(A, s, spv, Ms, invZ);
+        A.coef[((uint32_t)i << A.kshift) | (uint32_t)j] = make_float2(score_alpha<SK>(c, R, lp, gT[j], A.pw), R);
+        bin_key(A, ids[j], ((uint32_t)i << A.kshift) | (uint32_t)j);
+      }
+    }
+  }
+  lfin = wave_sum(lfin);
+  if (lane == 0) s_st[wv * 8 + 2] = lfin;   // (merge state already consumed)
+  if (A.train && tid < nValid * 3 && (A.rel_dests || tid % 3 != 2)) {
+    const int p = tid / 3, c = tid % 3;
+    const int64_t dest = c == 0 ? s_pos[p * 3] : c == 1 ? s_pos[p * 3 + 2] : A.ent.rows + s_pos[p * 3 + 1];
+    bin_key(A, dest, A.nkeyneg + (((uint32_t)(i0 + p)) << 2) + (uint32_t)c);
+  }
+  if (err) set_status(A.status, err);
+  KGE_PROF(4);
+  __syncthreads();
+
+  // ---- workgroup partials; the last workgroup to finish reduces them in a
+  // fixed order and publishes the clip scales and the loss
+  if (tid == 0) {
+    float wl;   // weight of a wave's summed negative loss terms (loss.py)
+    switch (A.loss_kind) {
+      case KGE_LOSS_HINGE: wl = A.inv_bk; break;
+      case KGE_LOSS_LOGISTIC: wl = 1.f; break;
+      case KGE_LOSS_SANS: case KGE_LOSS_BCE: wl = -A.inv_b; break;
+      default: wl = 0.5f * A.inv_b; break;
+    }
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < nValid; ++p) {
+      const float* mg = s_mrg + p * MG_STRIDE;
+      float lneg = 0.f;
+      for (int g = 0; g < wpp; ++g) lneg += s_st[(p * wpp + g) * 8 + 2];
+      acc[0] += mg[MG_LOSS] + wl * lneg;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[1 + v] += mg[MG_N + v];
+    }
+    // publish: write-through (agent-scope) stores, drained before the ticket
+    // add -- no L2 write-back fence (MI355X: one per workgroup is costly)
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      __hip_atomic_store(&A.part[(int64_t)blockIdx.x * 8 + k], acc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);   // vmcnt / lgkmcnt / expcnt drained
+    const uint32_t prev = __hip_atomic_fetch_add(&A.ctl->score_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (uint32_t)(gridDim.x - 1);
+  }
+  __syncthreads();
+  if (s_last) {
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int w = tid; w < (int)gridDim.x; w += blockDim.x) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        acc[k] += __hip_atomic_load(&A.part[(int64_t)w * 8 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) acc[k] = wave_sum(acc[k]);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s_misc[wv * 8 + k] = acc[k];
+    }
+    __syncthreads();
+    if (tid < 5) {
+      float s = 0.f;
+      for (int w = 0; w < W; ++w) s += s_misc[w * 8 + tid];
+      if (tid == 0) {
+        A.loss_out[0] = s;
+        if (A.loss_accum) A.loss_accum[0] += s;
+        A.ctl->loss = s;
+        A.ctl->score_ticket = 0u;
+        // every workgroup's keys are filed: hand the overflow length to the
+        // update kernel and restart the overflow list for the next step
+        A.ctl->ovf_len = __hip_atomic_exchange(&A.ctl->ovf_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        A.ctl->scale[tid - 1] = -A.lr * (A.clip_norm / fmaxf(sqrtf(s), A.clip_norm));
+        if (A.norm2_out) A.norm2_out[tid - 1] = s;
+      }
+    }
+  }
+  KGE_PROF(5);
+}
+
+// ------------------------------------------------------------ KU update
+// Destination-major: one wave per destination row (entities [0, E), then
+// relations [E, E + R)). The wave reads its list of codes (filed in arrival
+// order by the score kernel) and visits them in ascending code order -- so
+// every row is summed in the same order on every run (bit-reproducible, no
+// float atomics). It re-derives each negative's row gradient from ONE
+// frozen context row + its coefficient, adds the positives' own row
+// gradients, and applies clip_by_norm(5) per variable (BaseModel.py:327;
+// TF-2.5 IndexedSlices: norm over un-deduplicated slices, reduced by the
+// score kernel) and the SGD update (BaseModel.py:328, keras SGD
+// ResourceScatterAdd) with ONE read-modify-write per touched row. The
+// destination's counter is cleared for the next step as it is read.
+template <template <int, int, int> class Model, int VEC, int NC, int SK>
+__global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
+  using M = Model<VEC, NC, SK>;
+  using F = Frag<VEC, NC>;
+  constexpr int U = KGE_UPDATE_U / NC > 1 ? KGE_UPDATE_U / NC : 2;   // entries in flight per wave
+  constexpr int RV = RelV<M::CPLX, VEC>::n;
+  constexpr int CHMAX = 4;                            // in-register ordering up to 256 codes
+  __shared__ uint32_t s_scr[kUpdWaves][CHMAX * KGE_WAVE];
+
+  KGE_PROF_INIT();
+  const int lane = lane_id(), wv = wave_id();
+  const int64_t E_ = A.ent.rows;
+  // relation rows first: few rows with the longest lists (every positive
+  // files one), so they start early instead of forming the kernel's tail
+  const int64_t R_ = A.rel_dests ? A.rel.rows : 0;
+  const int64_t ndest = E_ + R_;
+  const int64_t dd = (int64_t)blockIdx.x * kUpdWaves + wv;
+  const int64_t d = dd < R_ ? E_ + dd : dd - R_;
+  const uint32_t nneg = A.nkeyneg;
+  const uint32_t kmask = (1u << A.kshift) - 1u;
+  const uint32_t snap_stride = (uint32_t)(M::NSNAP * A.snap_cols);   // B * stride < 2^32 (plan check)
+  const float sc_ent = A.ctl->scale[0], sc_rel = A.ctl->scale[1];   // issued up front
+
+  // one code -> its positive i and slot j (negative, c = -1) or row part c (0 h, 1 t, 2 r)
+  auto decode = [&](uint32_t code, int64_t* i, int* j, int* c) {
+    if (code < nneg) {
+      *i = code >> A.kshift;
+      *j = (int)(code & ((1u << A.kshift) - 1u));
+      *c = -1;
+    } else {
+      *i = (code - nneg) >> 2;
+      *j = 0;
+      *c = (int)((code - nneg) & 3u);
+    }
+  };
+  // entity destination: add the gradient rows of `cntv` (<= U) entries
+  float accE = 0.f;   // LINEAR_E models: summed coefficient of the destination row itself
+  auto entity_add = [&](const uint32_t* codes, int cntv, const F& E, F& acc) {
+    int64_t ii[U];
+    int jj[U], cc[U];
+    typename M::ECtx ec[U];   // a positive's own row gradient goes into ec[u].c0
+    float2 cf[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < cntv) {
+        decode(codes[u], &ii[u], &jj[u], &cc[u]);
+        if (cc[u] < 0) {
+          cf[u] = A.coef[codes[u]];
+          M::load_ectx(A.snap + ii[u] * (M::NSNAP * (int64_t)A.snap_cols), A.snap_cols,
+                       slot_kind(A.side_mode, jj[u]), ec[u]);
+        } else {
+          load_row(ec[u].c0, A.gpe + ii[u] * (int64_t)A.gpe_stride + (cc[u] == 0 ? 0 : A.gpe_toff), A.ent.cols);
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < cntv) {
+        if (cc[u] < 0) {
+          if constexpr (M::LINEAR_E) {
+            // g = alpha_E * E + alpha_C * c0: wave-uniform scalars, one FMA per element
+            float aE, aC;
+            M::lin_coefs(slot_kind(A.side_mode, jj[u]), cf[u].x, aE, aC);
+            accE += aE;
+#pragma unroll
+            for (int q = 0; q < VEC * NC; ++q) acc.v[q] += aC * ec[u].c0.v[q];
+          } else {
+            F g;
+            M::grad_entity(ec[u], slot_kind(A.side_mode, jj[u]), E, cf[u].x, cf[u].y, g);
+            add_to(acc, g);
+          }
+        } else {
+          add_to(acc, ec[u].c0);
+        }
+      }
+    }
+  };
+  auto rel_add = [&](const uint32_t* codes, int cntv, float (&acc)[RV * NC]) {
+    float g[U][RV * NC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < cntv) {
+        int64_t ii;
+        int jj, cc;
+        decode(codes[u], &ii, &jj, &cc);
+        load_rel_row<M::CPLX, VEC, NC>(g[u], A.gpos + ii * 3 * (int64_t)A.gcols + A.gcols, A.rel_gcols);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (u < cntv) {
+#pragma unroll
+        for (int q = 0; q < RV * NC; ++q) acc[q] += g[u][q];
+      }
+  };
+
+  float dn2 = 0.f;   // dense mode: this wave's ||summed row gradient||^2
+  if (dd < ndest) {
+    const bool is_ent = d < E_;
+    const uint32_t* lst = A.list + d * (int64_t)A.cap;
+    // issued together: the counter, the list's first 64 entries (speculative;
+    // lanes past the count are ignored) and the entity row
+    const uint32_t n = A.cnt[d];
+    const uint32_t code0 = lst[min(lane, A.cap - 1)];
+    F E, acc;
+    acc.zero();
+    E.zero();
+    // an untouched row is read only when the step rewrites it anyway (fused
+    // constraint) or it carries a dense term
+    if (is_ent && (n != 0u || A.fuse_norm || A.dense)) {
+      load_row(E, A.ent.row(d), A.ent.cols);
+      if (A.fuse_norm) {
+        normalize_row(E);   // the step's constraint assign, then this step's update
+        if (n == 0u) store_row(E, A.ent.row_w(d), A.ent.cols);
+      }
+    }
+    if (n != 0u || (A.dense && is_ent)) {
+      if (lane == 0 && n != 0u) A.cnt[d] = 0u;   // ready for the next step
+      float racc[RV * NC];
+#pragma unroll
+      for (int q = 0; q < RV * NC; ++q) racc[q] = 0.f;
+      auto consume_sorted = [&](auto code_at) {
+        int p0 = 0;
+        if constexpr (M::LINEAR_E) {
+          if (is_ent) {
+            // the negatives come first in code order: U-wide batches with no
+            // per-entry branches (padding entries repeat a code with weight 0)
+            int nn = 0;   // negatives among the n codes (binary search on the sorted codes)
+            {
+              int lo = 0, hi = (int)n;
+              while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (code_at(mid) < nneg) lo = mid + 1; else hi = mid;
+              }
+              nn = lo;
+            }
+            for (; p0 < nn; p0 += U) {
+              typename M::ECtx ec[U];
+              float2 cf[U];
+              int kd[U];
+#pragma unroll
+              for (int u = 0; u < U; ++u) {
+                const uint32_t code = code_at(min(p0 + u, nn - 1));
+                const uint32_t i = code >> A.kshift;
+                kd[u] = slot_kind(A.side_mode, (int)(code & kmask));
+                cf[u] = A.coef[code];
+                M::load_ectx(A.snap + i * snap_stride, A.snap_cols, kd[u], ec[u]);
+              }
+#pragma unroll
+              for (int u = 0; u < U; ++u) {
+                float aE, aC;
+                M::lin_coefs(kd[u], p0 + u < nn ? cf[u].x : 0.f, aE, aC);
+                accE += aE;
+#pragma unroll
+                for (int q = 0; q < VEC * NC; ++q) acc.v[q] += aC * ec[u].c0.v[q];
+              }
+            }
+            p0 = nn;
+          }
+        }
+        for (; p0 < (int)n; p0 += U) {
+          uint32_t cs[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) cs[u] = code_at(min(p0 + u, (int)n - 1));
+          if (is_ent) entity_add(cs, min(U, (int)n - p0), E, acc);
+          else rel_add(cs, min(U, (int)n - p0), racc);
+        }
+      };
+      if (n == 0u) {
+        // dense mode, untouched row: the regulariser term only
+      } else if (n <= (uint32_t)A.cap && n <= (uint32_t)KGE_WAVE) {
+        // ascending code order: each code's rank among the n (codes are
+        // unique), then a forward permute puts code of rank r in lane r
+        const uint32_t code = lane < (int)n ? code0 : 0xFFFFFFFFu;
+        uint32_t rank = 0u;
+        for (int q = 0; q < (int)n; ++q) rank += ((uint32_t)__builtin_amdgcn_readlane((int)code, q) < code) ? 1u : 0u;
+        const int sorted = __builtin_amdgcn_ds_permute((int)(min(rank, 63u) << 2), (int)code);
+        consume_sorted([&](int p) { return (uint32_t)__builtin_amdgcn_readlane(sorted, p); });
+      } else if (n <= (uint32_t)A.cap && n <= (uint32_t)(CHMAX * KGE_WAVE)) {
+        const int nch = (int)((n + KGE_WAVE - 1) / KGE_WAVE);
+        uint32_t code[CHMAX];
+#pragma unroll
+        for (int c = 0; c < CHMAX; ++c) {
+          const uint32_t q = (uint32_t)(c * KGE_WAVE + lane);
+          code[c] = (c < nch && q < n) ? lst[q] : 0xFFFFFFFFu;
+        }
+        uint32_t rank[CHMAX] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int c2 = 0; c2 < CHMAX; ++c2) {
+          if (c2 < nch) {
+            const int lim = min(KGE_WAVE, (int)n - c2 * KGE_WAVE);
+            for (int q = 0; q < lim; ++q) {
+              const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)code[c2], q);
+#pragma unroll
+              for (int c = 0; c < CHMAX; ++c) rank[c] += (o < code[c]) ? 1u : 0u;
+            }
+          }
+        }
+        uint32_t* scr = s_scr[wv];
+#pragma unroll
+        for (int c = 0; c < CHMAX; ++c)
+          if (c < nch && (uint32_t)(c * KGE_WAVE + lane) < n) scr[rank[c]] = code[c];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        consume_sorted([&](int p) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)scr[p]); });
+      } else {
+        // a list past its capacity: repeated selection of the next code from
+        // the list and the overflow entries (correct for any skew, not fast)
+        const uint32_t nl = min(n, (uint32_t)A.cap);
+        const uint32_t novf = A.ctl->ovf_len;
+        uint32_t last = 0u;
+        for (uint32_t p = 0; p < n; ++p) {
+          uint32_t best = 0xFFFFFFFFu;
+          for (uint32_t q = lane; q < nl; q += KGE_WAVE) {
+            const uint32_t x = lst[q];
+            if ((p == 0u || x > last) && x < best) best = x;
+          }
+          for (uint32_t q = lane; q < novf; q += KGE_WAVE) {
+            const uint64_t y = A.ovf[q];
+            const uint32_t x = (uint32_t)y;
+            if ((int64_t)(y >> 32) == d && (p == 0u || x > last) && x < best) best = x;
+          }
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, KGE_WAVE));
+          last = best;
+          uint32_t cs[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) cs[u] = best;
+          if (is_ent) entity_add(cs, 1, E, acc);
+          else rel_add(cs, 1, racc);
+        }
+      }
+      if (is_ent) {
+        if constexpr (M::LINEAR_E) {
+#pragma unroll
+          for (int q = 0; q < VEC * NC; ++q) acc.v[q] += accE * E.v[q];
+        }
+        if (A.dense) {
+#pragma unroll
+          for (int q = 0; q < VEC * NC; ++q) acc.v[q] += A.dense_ent * E.v[q];
+          dn2 = sq_partial(acc);
+        }
+        if (A.grad_mode || A.dense) {
+          store_row(acc, A.gent + d * (int64_t)A.ent.cols, A.ent.cols);
+        } else {
+#pragma unroll
+          for (int q = 0; q < VEC * NC; ++q) E.v[q] = E.v[q] + acc.v[q] * sc_ent;
+          store_row(E, A.ent.row_w(d), A.ent.cols);
+        }
+      } else {
+        const int64_t r = d - E_;
+        if (A.grad_mode) {
+          store_rel_row<M::CPLX, VEC, NC>(racc, A.grel + r * (int64_t)A.rel_gcols, A.rel.cols);
+        } else {
+          float row[RV * NC];
+          load_rel_row<M::CPLX, VEC, NC>(row, A.rel.row(r), A.rel.cols);
+#pragma unroll
+          for (int q = 0; q < RV * NC; ++q) row[q] = row[q] + racc[q] * sc_rel;
+          store_rel_row<M::CPLX, VEC, NC>(row, A.rel.row_w(r), A.rel.cols);
+        }
+      }
+    }
+  }
+  if (A.dense) {
+    // ||dense gradient||^2: workgroup partial, the last workgroup reduces
+    // every partial in a fixed order (clip_by_norm of the dense tensor)
+    __shared__ float s_n2[kUpdWaves];
+    __shared__ int s_lastu;
+    dn2 = wave_sum(dn2);
+    if (lane == 0) s_n2[wv] = dn2;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float w = 0.f;
+      for (int k = 0; k < kUpdWaves; ++k) w += s_n2[k];
+      __hip_atomic_store(&A.upart[blockIdx.x], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0);
+      const uint32_t prev = __hip_atomic_fetch_add(&A.ctl->upd_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_lastu = prev == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (s_lastu) {
+      float acc2 = 0.f;
+      for (int w = threadIdx.x; w < (int)gridDim.x; w += blockDim.x)
+        acc2 += __hip_atomic_load(&A.upart[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      acc2 = wave_sum(acc2);
+      if (lane == 0) s_n2[wv] = acc2;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int k = 0; k < kUpdWaves; ++k) t += s_n2[k];
+        A.ctl->dn2[0] = t;
+        if (A.norm2_out) A.norm2_out[0] = t;
+        A.ctl->upd_ticket = 0u;
+      }
+    }
+  }
+  KGE_PROF(16);
+}
+
+// ------------------------------------------------------------ dispatch
+template <template <int, int, int> class Model, int VEC, int NC, int SK>
+static void launch_score(const StepArgs& A, const StepGeom& G, hipStream_t st) {
+#ifdef KGE_ONLY_ONE
+  hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK, KGE_SIDE_HT>), dim3(G.nWG), dim3(kStepThreads), G.lds_score,
+                     st, A);
+#else
+  if (A.side_mode == KGE_SIDE_HT)
+    hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK, KGE_SIDE_HT>), dim3(G.nWG), dim3(kStepThreads), G.lds_score,
+                       st, A);
+  else if (A.side_mode == KGE_SIDE_H)
+    hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK, KGE_SIDE_H>), dim3(G.nWG), dim3(kStepThreads), G.lds_score,
+                       st, A);
+  else
+    hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK, KGE_SIDE_T>), dim3(G.nWG), dim3(kStepThreads), G.lds_score,
+                       st, A);
+#endif
+}
+
+template <template <int, int, int> class Model, int VEC, int NC, int SK>
+static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_t st, hipEvent_t const* ev) {
+  launch_score<Model, VEC, NC, SK>(A, G, st);
+  if (ev) (void)hipEventRecord(ev[2], st);
+  if (A.train)
+    hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
+  return KGE_OK;
+}
+
+#ifndef KGE_ONLY_ONE
+template <template <int, int, int> class Model, int VEC, int NC>
+static kge_status by_sk(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st, hipEvent_t const* ev) {
+  switch (sk) {
+    case SK_P1: return launch_family<Model, VEC, NC, SK_P1>(A, G, st, ev);
+    case SK_P2: return launch_family<Model, VEC, NC, SK_P2>(A, G, st, ev);
+    case SK_PINF: return launch_family<Model, VEC, NC, SK_PINF>(A, G, st, ev);
+    default: return launch_family<Model, VEC, NC, SK_DOT>(A, G, st, ev);
+  }
+}
+
+template <template <int, int, int> class Model, int VEC, int NC>
+static kge_status by_sk_lp(const StepArgs& A, const StepGeom& G, int sk, hipStream_t st, hipEvent_t const* ev) {
+  switch (sk) {
+    case SK_P1: return launch_family<Model, VEC, NC, SK_P1>(A, G, st, ev);
+    case SK_P2: return launch_family<Model, VEC, NC, SK_P2>(A, G, st, ev);
+    case SK_PINF: return launch_family<Model, VEC, NC, SK_PINF>(A, G, st, ev);
+    default: return KGE_EUNSUPPORTED;
+  }
+}
+
+#endif  // KGE_ONLY_ONE
+
+}  // namespace kge

@@ -1,0 +1,39 @@
+// RESCAL instances of the fused step kernels (RESCAL.py:140-200); the
+// relation-matrix MFMA passes live in kge_rel.hip.
+#include "kge_step_impl.h"
+
+namespace kge {
+
+#ifndef KGE_ONLY_ONE
+// RESCAL: context pass -> score (dot products against u / v) -> regulariser
+// loss -> projection + dR pass -> update kernel (dense entity gradient)
+template <int VEC, int NC>
+static kge_status rescal_vn(const StepArgs& A, const StepGeom& G, const RelArgs& P, float lam, float* regpart,
+                            hipStream_t st, hipEvent_t const* ev) {
+  launch_rel_rank(P, st);
+  launch_rel_ctx(P, st);
+  launch_score<Rescal, VEC, NC, SK_DOT>(A, G, st);
+  if (lam != 0.f) launch_reg_loss(A.ent, A.rel, lam, regpart, A.ctl, A.loss_out, A.loss_accum, st);
+  if (ev) (void)hipEventRecord(ev[2], st);
+  if (A.train) {
+    launch_rel_post(P, st);
+    hipLaunchKernelGGL((update_kernel<Rescal, VEC, NC, SK_DOT>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
+  }
+  return KGE_OK;
+}
+
+kge_status launch_step_rescal(const StepArgs& A, const StepGeom& G, const RelArgs& P, float lam, float* regpart,
+                              hipStream_t st, hipEvent_t const* ev) {
+  if (G.vec == 4) {
+    if (G.nc == 1) return rescal_vn<4, 1>(A, G, P, lam, regpart, st, ev);
+    if (G.nc == 2) return rescal_vn<4, 2>(A, G, P, lam, regpart, st, ev);
+    return rescal_vn<4, 4>(A, G, P, lam, regpart, st, ev);
+  }
+  if (G.nc == 1) return rescal_vn<1, 1>(A, G, P, lam, regpart, st, ev);
+  if (G.nc == 2) return rescal_vn<1, 2>(A, G, P, lam, regpart, st, ev);
+  return rescal_vn<1, 4>(A, G, P, lam, regpart, st, ev);
+}
+#endif  // KGE_ONLY_ONE
+
+
+}  // namespace kge

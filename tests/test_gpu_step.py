@@ -27,6 +27,7 @@ def _dev():
 
 def _make(model_name, d, K, side, score_fn, loss_fn, E, R, sampler, constraint=True):
     from KGE.models.semantic_based.DistMult import DistMult
+    from KGE.models.semantic_based.RESCAL import RESCAL
     from KGE.models.translating_based.RotatE import RotatE
     from KGE.models.translating_based.TransE import TransE
     common = dict(loss_fn=loss_fn, ns_strategy=sampler)
@@ -34,6 +35,8 @@ def _make(model_name, d, K, side, score_fn, loss_fn, E, R, sampler, constraint=T
         m = TransE({"embedding_size": d}, K, side, score_fn=score_fn, constraint=constraint, **common)
     elif model_name == "RotatE":
         m = RotatE({"embedding_size": d}, K, side, score_fn=score_fn, **common)
+    elif model_name == "RESCAL":
+        m = RESCAL({"embedding_size": d}, K, side, constraint=constraint, constraint_weight=0.5, **common)
     else:
         m = DistMult({"embedding_size": d}, K, side, constraint=constraint, **common)
     m.metadata = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
@@ -44,6 +47,9 @@ def _weights(model_name, E, R, d, rng):
     if model_name == "RotatE":
         return {"ent_emb": rng.uniform(-0.5, 0.5, (E, d, 2)).astype(np.float32),
                 "rel_emb": rng.uniform(-0.5, 0.5, (R, d)).astype(np.float32)}
+    if model_name == "RESCAL":
+        return {"ent_emb": rng.uniform(-0.5, 0.5, (E, d)).astype(np.float32),
+                "rel_inter": rng.uniform(-0.2, 0.2, (R, d, d)).astype(np.float32)}
     rk = "rel_inter" if model_name == "DistMult" else "rel_emb"
     return {"ent_emb": rng.uniform(-0.5, 0.5, (E, d)).astype(np.float32),
             rk: rng.uniform(-0.5, 0.5, (R, d)).astype(np.float32)}
@@ -102,9 +108,9 @@ def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, id
                         sampler="typed" if typed is not None else "uniform", typed=tt)
     lim = getattr(m, "limit", None)
     ref = orc.train_step(model_name, W, pos, neg, score=_spec_score(getattr(m, "score_fn", None))
-                         if model_name != "DistMult" else ("dot", 0.0), loss=_spec_loss(loss_fn), lr=lr,
-                         constraint=constraint if model_name != "RotatE" else False, side=side, train=train,
-                         limit=lim, optimizer=opt)
+                         if model_name not in ("DistMult", "RESCAL") else ("dot", 0.0), loss=_spec_loss(loss_fn),
+                         lr=lr, constraint=constraint if model_name != "RotatE" else False, side=side, train=train,
+                         limit=lim, optimizer=opt, constraint_weight=getattr(m, "constraint_weight", 1.0))
     got = {k: v.cpu().numpy() for k, v in m.model_weights.items()}
     return ref, got, float(step.loss_out.item()), ps.cpu().numpy(), ns.cpu().numpy(), step, neg
 
@@ -164,6 +170,36 @@ def test_rotate(hiplib, si, d):
     s = _scores()[si]
     ref, got, l_, ps, ns, _, _ = run_case(hiplib, "RotatE", d, 7, 6, "h+t", s,
                                           loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0))
+    check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("li", range(5))
+@pytest.mark.parametrize("side", ["h+t", "t"])
+def test_rescal(hiplib, li, side):
+    """RESCAL (MFMA context / projection / dR passes + dot-product stream):
+    R = 3 relations over 40 positives, so relation groups span several
+    16-positive tiles; d = 24 pads the 16-wide MFMA tiles."""
+    ref, got, loss, ps, ns, _, _ = run_case(hiplib, "RESCAL", 24, 40, 6, side, None, _losses()[li], R=3)
+    check(ref, got, loss, ps, ns)
+
+
+@pytest.mark.parametrize("d,B,K,R", [(200, 24, 64, 5), (64, 70, 4, 2), (17, 9, 3, 12)])
+def test_rescal_shapes(hiplib, d, B, K, R):
+    """C4's RESCAL shape at reduced batch (d = 200, K = 64), a 35-positive
+    relation group, and an odd d with more relations than positives."""
+    from KGE import loss
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "RESCAL", d, B, K, "h+t", None, loss.SquareErrorLoss(), R=R,
+                                          E=300)
+    check(ref, got, l_, ps, ns)
+
+
+def test_rescal_validation_and_adam(hiplib):
+    from KGE import loss
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "RESCAL", 32, 12, 4, "h+t", None, loss.SquareErrorLoss(),
+                                          train=False)
+    check(ref, got, l_, ps, ns)
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "RESCAL", 32, 12, 4, "h+t", None,
+                                          loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), opt="adam", lr=0.01)
     check(ref, got, l_, ps, ns)
 
 
