@@ -63,10 +63,43 @@ def fused_plan(model, optimizer):
         return "custom negative sampler"
     if optimizer is not None and not isinstance(optimizer, (_opt.SGD, _opt.Adam)):
         return "%s optimizer has no fused apply" % type(optimizer).__name__
-    return None
+    return _native_plan_error(model, optimizer)
 
 
-FUSED_MODELS = (_hip.MODEL_TRANSE, _hip.MODEL_DISTMULT, _hip.MODEL_ROTATE, _hip.MODEL_RESCAL)
+def _native_plan_error(model, optimizer):
+    """Ask the library whether it has an instance for this combination
+    (``kge_step_workspace_bytes`` is 0 for a plan it cannot run, with the
+    reason in ``kge_last_error``: rows wider than the fragment limit, LDS
+    budget, RESCAL without its regulariser, ...). Cached per configuration."""
+    try:
+        t = model._fused_tables()
+    except (AttributeError, KeyError):
+        return None
+    if t["ent"].device.type != "cuda":
+        return None      # FusedStep raises: the fused step needs the model on a GPU
+    key = (tuple(t["ent"].shape), tuple(t["rel"].shape), type(optimizer).__name__, model.negative_ratio,
+           model.corrupt_side, bool(getattr(model, "constraint", False)),
+           _score.fused_descriptor(model.score_fn) if hasattr(model, "score_fn") else None,
+           _loss.fused_descriptor(model.loss_fn))
+    cache = model.__dict__.setdefault("_native_plan_cache", {})
+    if key not in cache:
+        lib = _hip.lib()      # raises if libkge_hip.so is missing (no silent fallback)
+        probe = FusedStep(model)
+        dev = t["ent"].device
+        batch = torch.zeros((1, 3), dtype=torch.int64, device=dev)
+        neg = torch.zeros(max(int(model.negative_ratio), 1), dtype=torch.int64, device=dev)
+        train = optimizer is not None
+        # the SGD form of the plan (an Adam probe would allocate dense gradients)
+        opt = optimizer if isinstance(optimizer, _opt.SGD) or not train else _opt.SGD(0.01)
+        d = probe.describe(batch, train, opt, neg_ids=neg)
+        if int(lib.kge_step_workspace_bytes(d)) == 0:
+            cache[key] = "kge_step: " + lib.kge_last_error().decode(errors="replace")
+        else:
+            cache[key] = None
+    return cache[key]
+
+
+FUSED_MODELS = (_hip.MODEL_TRANSE, _hip.MODEL_DISTMULT, _hip.MODEL_ROTATE, _hip.MODEL_RESCAL, _hip.MODEL_TRANSR)
 
 
 def fused_names(model):
@@ -119,12 +152,17 @@ class FusedStep:
     def _tables(self):
         return self.tables if self.tables is not None else self.model._fused_tables()
 
+    def grad_roles(self):
+        """Variables of the step in grad_out / norm2_out order (kge_hip.h)."""
+        t = self._tables()
+        return [r for r in ("ent", "rel", "rel_aux", "ent_aux") if t.get(r) is not None]
+
     def grad_buffers(self):
-        """Dense [rows, cols] gradient buffers of the ent / rel tables (KGE_OPT_GRAD)."""
+        """Dense [rows, cols] gradient buffers of the step's tables (KGE_OPT_GRAD)."""
         if self.grads is None:
             t = self._tables()
             self.grads = [torch.zeros(_rows_cols(t[k]), dtype=torch.float32, device=self.device)
-                          for k in ("ent", "rel")]
+                          for k in self.grad_roles()]
         return self.grads
 
     def _opt_code(self, is_train, optimizer):
@@ -187,8 +225,9 @@ class FusedStep:
         d.flags = self.flags
         if d.optimizer == _hip.OPT_GRAD:
             g = self.grad_buffers()
-            d.grad_out[0] = g[0].data_ptr()
-            d.grad_out[1] = g[1].data_ptr()
+            slot = {"ent": 0, "rel": 1, "rel_aux": 2, "ent_aux": 3}
+            for role, buf in zip(self.grad_roles(), g):
+                d.grad_out[slot[role]] = buf.data_ptr()
         d.loss_out = self.loss_out.data_ptr()
         d.loss_accum = self.loss_accum.data_ptr()
         d.norm2_out = self.norm2.data_ptr()
@@ -267,8 +306,9 @@ class FusedStep:
         t = self._tables()
         names = fused_names(self.model)
         g = self.grad_buffers()
-        for v, role in enumerate(("ent", "rel")):
-            self.apply(t[role], g[v], self.norm2.data_ptr() + 4 * v, optimizer, names[role])
+        slot = {"ent": 0, "rel": 1, "rel_aux": 2, "ent_aux": 3}
+        for role, buf in zip(self.grad_roles(), g):
+            self.apply(t[role], buf, self.norm2.data_ptr() + 4 * slot[role], optimizer, names[role])
 
     def check_status(self):
         _hip.check_device_status(self.status, "kge_step")

@@ -52,6 +52,11 @@ class TransR(TranslatingModel):
         assert list(model_weights["rel_emb"].shape) == [R, kr], "shape of 'rel_emb' should be (len(metadata['ind2rel']), embedding_params['rel_embedding_size'])"
         assert list(model_weights["rel_proj"].shape) == [R, ke, kr], "shape of 'rel_emb' should be (len(metadata['ind2rel']), embedding_params['ent_embedding_size'], embedding_params['rel_embedding_size'])"
 
+    def _fused_tables(self):
+        return {"ent": self.model_weights["ent_emb"], "rel": self.model_weights["rel_emb"],
+                "rel_aux": self.model_weights["rel_proj"], "dim": self.embedding_params["ent_embedding_size"],
+                "dim_rel": self.embedding_params["rel_embedding_size"]}
+
     def score_hrt(self, h, r, t):
         """``TransR.py:154-191``."""
         h, r, t = super(TransR, self).score_hrt(h, r, t)

@@ -47,7 +47,8 @@ struct Plan {
   uint64_t o_ctl, o_cnt, o_coef, o_snap, o_gpos, o_part, o_list, o_ovf;
   // dense-gradient / relation-matrix models (RESCAL)
   uint64_t o_upart, o_sorted, o_srel, o_gproj, o_rpart, o_regpart, o_gent, o_grel;
-  bool rescal;
+  uint64_t o_gneg, o_dm;   // TransR
+  bool rescal, transr;
 };
 
 int score_sk(int kind, float p) {
@@ -71,12 +72,14 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     return fail(KGE_EINVAL, "abi_version %d != library %d", d->abi_version, KGE_ABI_VERSION);
   const int model = d->model;
   if (model != KGE_MODEL_TRANSE && model != KGE_MODEL_DISTMULT && model != KGE_MODEL_ROTATE &&
-      model != KGE_MODEL_RESCAL)
+      model != KGE_MODEL_RESCAL && model != KGE_MODEL_TRANSR)
     return fail(KGE_EUNSUPPORTED, "model %d has no fused kernel in this build", model);
   if (d->dim <= 0) return fail(KGE_EINVAL, "dim must be > 0");
-  const bool rescal = model == KGE_MODEL_RESCAL;
+  const bool rescal = model == KGE_MODEL_RESCAL, transr = model == KGE_MODEL_TRANSR;
   const int64_t entc = model == KGE_MODEL_ROTATE ? 2 * (int64_t)d->dim : d->dim;
-  const int64_t relc = rescal ? (int64_t)d->dim * d->dim : d->dim;   // RESCAL: [R, d, d] matrices
+  // RESCAL: [R, d, d] matrices; TransR: rel_emb [R, k] (+ rel_proj [R, d, k] in rel_aux)
+  const int64_t relc = rescal ? (int64_t)d->dim * d->dim : transr ? d->dim_rel : d->dim;
+  if (transr && d->dim_rel <= 0) return fail(KGE_EINVAL, "dim_rel must be > 0");
   kge_status s;
   if ((s = check_table(d->ent, "ent_emb", entc))) return s;
   if ((s = check_table(d->rel, (model == KGE_MODEL_DISTMULT || rescal) ? "rel_inter" : "rel_emb", relc))) return s;
@@ -87,6 +90,12 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     if (!d->constraint)
       return fail(KGE_EUNSUPPORTED, "RESCAL with constraint=False (slice-norm clipping) has no fused kernel");
     if (d->dim > 256) return fail(KGE_EUNSUPPORTED, "RESCAL fused step supports d <= 256 (got %d)", d->dim);
+  }
+  if (transr) {
+    if ((s = check_table(d->rel_aux, "rel_proj", (int64_t)d->dim * d->dim_rel))) return s;
+    if (d->rel_aux.rows != d->rel.rows) return fail(KGE_EINVAL, "rel_proj rows != rel_emb rows");
+    if (d->dim > kTrMaxDim || d->dim_rel > kTrMaxDim)
+      return fail(KGE_EUNSUPPORTED, "TransR fused step supports embedding sizes <= %d", kTrMaxDim);
   }
   if (d->batch < 0) return fail(KGE_EINVAL, "batch must be >= 0");
   if (d->negative_ratio < 0) return fail(KGE_EINVAL, "negative_ratio must be >= 0");
@@ -111,6 +120,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   if (d->optimizer == KGE_OPT_SGD && !(d->clip_norm > 0.f)) return fail(KGE_EINVAL, "clip_norm must be > 0");
   if (d->optimizer == KGE_OPT_GRAD && (!d->grad_out[0] || !d->grad_out[1]))
     return fail(KGE_EINVAL, "KGE_OPT_GRAD needs grad_out[0] (ent) and grad_out[1] (rel)");
+  if (d->optimizer == KGE_OPT_GRAD && model == KGE_MODEL_TRANSR && !d->grad_out[2])
+    return fail(KGE_EINVAL, "KGE_OPT_GRAD needs grad_out[2] (rel_proj) for TransR");
   if (d->optimizer == KGE_OPT_GRAD && !d->norm2_out) return fail(KGE_EINVAL, "KGE_OPT_GRAD needs norm2_out");
   if (!d->loss_out) return fail(KGE_EINVAL, "null loss_out");
   const kge_sampler_desc& sm = d->sampler;
@@ -146,6 +157,14 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     vec = (entc % 4 == 0 && relc % 4 == 0 && d->ent.ld % 4 == 0 && d->rel.ld % 4 == 0 && a16) ? 4 : 1;
   }
   const int64_t rowlen = rescal ? entc : std::max(entc, relc);   // fragment row length
+  if (transr) {
+    const int Keff_ = d->corrupt_side == KGE_SIDE_HT ? 2 * (d->negative_ratio / 2) : d->negative_ratio;
+    if (Keff_ + 1 > kTrMaxSlots)
+      return fail(KGE_EUNSUPPORTED, "TransR fused step supports negative_ratio <= %d", kTrMaxSlots - 1);
+    const TrLds TL = tr_lds(d->dim, d->dim_rel, Keff_);
+    if ((size_t)TL.total_floats * 4 + 256 > 160 * 1024)
+      return fail(KGE_EUNSUPPORTED, "TransR LDS budget exceeded (%d bytes)", TL.total_floats * 4);
+  }
   const int nc = (int)ceil_div(rowlen, 64 * vec);
   if (nc > 4)
     return fail(KGE_EUNSUPPORTED, "row of %lld floats exceeds the fused kernel's %d", (long long)rowlen, 256 * vec);
@@ -187,6 +206,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.G.nWG = (int)nWG;
   P.G.gridU = (int)ceil_div(ndest, kUpdWaves);
   P.rescal = rescal;
+  P.transr = transr;
   P.G.lds_score = (size_t)SL.total;
   if (P.G.lds_score > 160 * 1024)
     return fail(KGE_EUNSUPPORTED, "LDS budget exceeded (score kernel %zu bytes)", P.G.lds_score);
@@ -248,14 +268,14 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
 
   uint64_t off = 0;
   auto take = [&](uint64_t bytes) { const uint64_t o = off; off += round_up((int64_t)bytes, 256); return o; };
-  const int nsnap = model == KGE_MODEL_ROTATE ? 3 : 2;
+  const int nsnap = model == KGE_MODEL_ROTATE ? 3 : transr ? 0 : 2;
   // zero-state words first: control block, per-destination counters
   P.o_ctl = take(sizeof(StepCtl));
   P.o_cnt = take((uint64_t)ndest * 4);
   P.o_coef = take((uint64_t)(B << kshift) * 8);   // indexed by destination code
   P.o_snap = take((uint64_t)B * nsnap * entc * 4);
   P.o_gpos = take((uint64_t)B * 3 * rowlen * 4);
-  P.o_part = take((uint64_t)nWG * 8 * 4);
+  P.o_part = take((uint64_t)(transr ? std::max<int64_t>(nWG, B) : nWG) * 8 * 4);   // TransR: one partial per positive
   P.o_list = take((uint64_t)ndest * cap * 4);
   P.o_ovf = take((uint64_t)T * 8);
   P.o_upart = take((uint64_t)P.G.gridU * 4);
@@ -270,6 +290,12 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
       P.o_gent = take((uint64_t)E * entc * 4);
       P.o_grel = take((uint64_t)R * relc * 4);
     }
+  }
+  if (transr) {
+    P.o_sorted = take((uint64_t)B * 4);
+    P.o_srel = take((uint64_t)B * 4);
+    P.o_gneg = take((uint64_t)(B << kshift) * entc * 4);
+    P.o_dm = take((uint64_t)B * d->dim * d->dim_rel * 4);
   }
   P.ws_bytes = std::max<uint64_t>(off, 256);
   return KGE_OK;
@@ -385,6 +411,26 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   A.gpe_stride = 3 * A.gcols;
   A.gpe_toff = 2 * A.gcols;
   RelArgs RA{};
+  TrArgs TA{};
+  if (P.transr) {
+    A.gneg = (float*)(ws + P.o_gneg);
+    RA.ent = A.ent;
+    RA.rel = A.rel;
+    RA.pos = A.pos;
+    RA.i64 = A.i64;
+    RA.B = A.B;
+    RA.sorted = (int32_t*)(ws + P.o_sorted);
+    RA.srel = (int32_t*)(ws + P.o_srel);
+    RA.status = A.status;
+    TA.proj = TabView{d->rel_aux.data, d->rel_aux.ld, (int32_t)(d->dim * d->dim_rel), d->rel_aux.rows};
+    TA.d = d->dim;
+    TA.k = d->dim_rel;
+    TA.clip = d->constraint != 0;
+    TA.dmpart = (float*)(ws + P.o_dm);
+    TA.sorted = RA.sorted;
+    TA.srel = RA.srel;
+    TA.gproj_out = d->optimizer == KGE_OPT_GRAD ? d->grad_out[2] : nullptr;
+  }
   if (P.rescal) {
     A.gpe = (float*)(ws + P.o_gproj);
     A.gpe_stride = 2 * d->dim;
@@ -415,6 +461,16 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   if (A.grad_mode && !P.rescal) {   // RESCAL's dense passes write every row
     (void)hipMemsetAsync(d->grad_out[0], 0, (size_t)A.ent.rows * A.ent.cols * sizeof(float), st);
     (void)hipMemsetAsync(d->grad_out[1], 0, (size_t)A.rel.rows * A.rel_gcols * sizeof(float), st);
+    if (P.transr) (void)hipMemsetAsync(d->grad_out[2], 0, (size_t)TA.proj.rows * TA.proj.cols * sizeof(float), st);
+  }
+  if (P.transr && d->constraint && !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT)) {
+    // _constraint_loss assigns (TransR.py:207-209): clip every entity and relation row to norm <= 1
+    const kge_table* tabs[2] = {&d->ent, &d->rel};
+    for (int v = 0; v < 2; ++v) {
+      const int64_t blocks = std::min<int64_t>(ceil_div(tabs[v]->rows, kWaves), 4096);
+      hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, tabs[v]->data,
+                         tabs[v]->rows, (int32_t)tabs[v]->cols, tabs[v]->ld, 1, 1.0f);
+    }
   }
   // _constraint_loss assigns before scoring (BaseModel.py:319): fused into
   // the score / update kernels on the SGD path (A.fuse_norm), else K0
@@ -430,7 +486,9 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     return hip_check("kge_step(empty batch)");
   }
   if (ev) (void)hipEventRecord(ev[1], st);
-  if (P.rescal) {
+  if (P.transr) {
+    s = launch_step_transr(A, P.G, TA, RA, P.sk, st, ev);
+  } else if (P.rescal) {
     s = launch_step_rescal(A, P.G, RA, d->constraint ? d->constraint_weight : 0.f,
                            (float*)(ws + P.o_regpart), st, ev);
     if (s == KGE_OK && d->optimizer == KGE_OPT_SGD) {

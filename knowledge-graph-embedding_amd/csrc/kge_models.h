@@ -208,6 +208,7 @@ struct MP {
 template <int VEC, int NC, int SK>
 struct TransE {
   static constexpr bool CPLX = false;
+  static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
   struct Ctx { F X, R, T, D; };
@@ -356,6 +357,7 @@ struct TransE {
 template <int VEC, int NC, int SK_UNUSED>
 struct DistMult {
   static constexpr bool CPLX = false;
+  static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
   struct Ctx { F H, R, T, HR, TR; };
@@ -436,6 +438,7 @@ struct DistMult {
 template <int VEC, int NC, int SK>
 struct RotatE {
   static constexpr bool CPLX = true;
+  static constexpr bool MAT = false;
   static constexpr int NSNAP = 3;
   static constexpr int HV = VEC / 2;
   using F = Frag<VEC, NC>;
@@ -568,6 +571,7 @@ struct RotatE {
 template <int VEC, int NC, int SK_UNUSED>
 struct Rescal {
   static constexpr bool CPLX = false;
+  static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
   struct Ctx { F H, T, U, V; };
@@ -623,6 +627,26 @@ struct Rescal {
 #pragma unroll
     for (int i = 0; i < VEC * NC; ++i) gE.v[i] = alpha * ec.c0.v[i];
   }
+};
+
+// ======================================================================
+// Materialised-gradient family (TransR; kge_transr.hip): the score pass
+// writes every negative's entity-row gradient to gneg[code] (it is a GEMM
+// output, M_r g, not a function of one context row), so the update kernel
+// only sums rows. Only the update-kernel hooks are defined.
+// ======================================================================
+template <int VEC, int NC, int SK_UNUSED>
+struct Materialised {
+  static constexpr bool CPLX = false;
+  static constexpr bool MAT = true;
+  static constexpr int NSNAP = 0;
+  static constexpr bool NRM_FROM_R = false;
+  static constexpr bool LINEAR_E = false;
+  using F = Frag<VEC, NC>;
+  struct ECtx { F c0; };
+  __device__ static void lin_coefs(int, float alpha, float& aE, float& aC) { aE = 0.f; aC = alpha; }
+  __device__ static void load_ectx(const float*, int, int, ECtx&) {}
+  __device__ static void grad_entity(const ECtx& ec, int, const F&, float, float, F& gE) { gE = ec.c0; }
 };
 
 }  // namespace kge

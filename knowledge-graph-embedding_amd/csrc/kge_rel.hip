@@ -32,15 +32,6 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// first sorted position in [lo, hi) whose relation is >= r
-__device__ __forceinline__ int64_t rel_lower(const int32_t* srel, int64_t lo, int64_t hi, int64_t r) {
-  while (lo < hi) {
-    const int64_t m = (lo + hi) >> 1;
-    if ((int64_t)srel[m] < r) lo = m + 1; else hi = m;
-  }
-  return lo;
-}
-
 __device__ __forceinline__ int64_t pos_id(const RelArgs& P, int64_t i, int c) {
   const int64_t v = load_idx(P.pos, i * 3 + c, P.i64);
   const int64_t lim = c == 1 ? P.rel.rows : P.ent.rows;

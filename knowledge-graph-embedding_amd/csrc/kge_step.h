@@ -63,6 +63,7 @@ struct StepArgs {
   float* gpe;
   int32_t gpe_stride, gpe_toff;
   float* upart;     // [gridU] update-kernel norm^2 partials (dense mode)
+  float* gneg;      // materialised family: [B << kshift, ent.cols] negatives' entity-row gradients
   // geometry
   int32_t wpp;      // waves per positive (1, 2, 4, 8)
   int32_t nP;       // positives per score workgroup = kStepWaves / wpp
@@ -133,6 +134,60 @@ void launch_rel_post(const RelArgs& R, hipStream_t st);     // g_h, g_t, dR (+ d
 void launch_reg_loss(const TabView& ent, const TabView& rel, float lam, float* part, StepCtl* ctl,
                      float* loss_out, float* loss_accum, hipStream_t st);
 constexpr int kRegWGs = 256;
+
+// first sorted position in [lo, hi) whose relation is >= r (srel ascending)
+__device__ __forceinline__ int64_t rel_lower(const int32_t* srel, int64_t lo, int64_t hi, int64_t r) {
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if ((int64_t)srel[m] < r) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+
+// ---- TransR (kge_transr.hip): one workgroup per positive, three MFMA products
+struct TrArgs {
+  TabView proj;      // rel_proj [R, d * k] (M_r row-major [d][k])
+  int32_t d, k;      // entity / relation embedding sizes
+  bool clip;         // constraint: projected vectors clipped to norm <= 1 (TransR.py:187-189)
+  float* dmpart;     // [B, d * k] per-positive dM partials (summed per relation by the apply pass)
+  const int32_t* sorted;
+  const int32_t* srel;
+  float* gproj_out;  // KGE_OPT_GRAD: dense [R, d * k] rel_proj gradient (else null)
+};
+constexpr int kTrWaves = 8;
+constexpr int kTrThreads = kTrWaves * KGE_WAVE;
+constexpr int kTrMaxSlots = 72;   // K + 1 slots over 8 waves, 9 per wave in registers
+constexpr int kTrMaxDim = 256;    // d, k (MFMA k-steps held in registers)
+// LDS carve of the TransR kernel (floats): X [NR16][LX] | P [NR16][LP], later
+// S [SR16][LP] over both; then per-row / per-slot scalars and partials
+struct TrLds {
+  int LX, LP, NR16, SR16;
+  int pn, xx, xh, xt, sS, sR, sT, sA, rp, ids, misc, total_floats;
+};
+__host__ __device__ inline TrLds tr_lds(int d, int k, int K) {
+  TrLds L;
+  L.LX = ((d + 3) & ~3) + 1;
+  L.LP = ((k + 3) & ~3) + 1;
+  L.NR16 = (K + 2 + 15) & ~15;
+  L.SR16 = (2 * K + 4 + 15) & ~15;
+  int o = L.NR16 * (L.LX + L.LP);
+  if (L.SR16 * L.LP + 16 > o) o = L.SR16 * L.LP + 16;   // + slack: GEMM3 reads whole 16-column tiles
+  L.pn = o; o += L.NR16;
+  L.xx = o; o += L.NR16;
+  L.xh = o; o += L.NR16;
+  L.xt = o; o += L.NR16;
+  L.sS = o; o += (K + 4) & ~3;
+  L.sR = o; o += (K + 4) & ~3;
+  L.sT = o; o += (K + 4) & ~3;
+  L.sA = o; o += (K + 4) & ~3;
+  L.rp = o; o += kTrWaves * L.LP;
+  L.ids = o; o += (K + 3) & ~3;
+  L.misc = o; o += 64;
+  L.total_floats = o;
+  return L;
+}
+kge_status launch_step_transr(const StepArgs& A, const StepGeom& G, const TrArgs& T, const RelArgs& P, int sk,
+                              hipStream_t st, hipEvent_t const* ev);
 kge_status launch_step_rescal(const StepArgs& A, const StepGeom& G, const RelArgs& P, float lam, float* regpart,
                               hipStream_t st, hipEvent_t const* ev);
 

@@ -673,9 +673,14 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
       if (u < cntv) {
         decode(codes[u], &ii[u], &jj[u], &cc[u]);
         if (cc[u] < 0) {
-          cf[u] = A.coef[codes[u]];
-          M::load_ectx(A.snap + ii[u] * (M::NSNAP * (int64_t)A.snap_cols), A.snap_cols,
-                       slot_kind(A.side_mode, jj[u]), ec[u]);
+          if constexpr (M::MAT) {
+            load_row(ec[u].c0, A.gneg + (int64_t)codes[u] * A.ent.cols, A.ent.cols);
+            cf[u] = make_float2(0.f, 0.f);
+          } else {
+            cf[u] = A.coef[codes[u]];
+            M::load_ectx(A.snap + ii[u] * (M::NSNAP * (int64_t)A.snap_cols), A.snap_cols,
+                         slot_kind(A.side_mode, jj[u]), ec[u]);
+          }
         } else {
           load_row(ec[u].c0, A.gpe + ii[u] * (int64_t)A.gpe_stride + (cc[u] == 0 ? 0 : A.gpe_toff), A.ent.cols);
         }

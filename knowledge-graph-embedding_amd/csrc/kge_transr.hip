@@ -1,0 +1,544 @@
+// TransR fused training step for gfx950 (TransR.py:154-211) on fp32 MFMA.
+//
+// TransR projects every entity row of a triple through its relation's
+// matrix M_r [d, k] before scoring:  s = score(clip(h M_r) + r, clip(t M_r)).
+// All triples of a positive share M_r, so the projection work of one
+// positive is three small GEMMs, done by ONE workgroup (8 waves):
+//
+//   X  [K+2, d]   its entity rows (h, t, the K negatives), gathered into LDS
+//   P  = X M_r    GEMM1 [K+2, d] x [d, k]     -> projected rows, clipped in place
+//   scores / loss / dL/dP per triple on the VALU (wave per slot); the
+//   per-triple gradients wrt every projected row (slices), back through the clip
+//   S  rows: summed h-slices, summed t-slices, each negative's slice, and
+//            every positive-side slice on its own (clip_by_norm sees slices)
+//   Y  = S M_r^T  GEMM2 [2K+4, k] x [k, d]  -> entity-row gradients (h, t to
+//                 the positive-gradient rows, negatives to gneg[code]) and
+//                 the entity slice norms ||M g||^2
+//   dM = X^T S'   GEMM3 [d, K+2] x [K+2, k] -> this positive's rel_proj
+//                 gradient (a per-positive partial; the apply pass sums a
+//                 relation's partials in positive order)
+//
+// MFMA: v_mfma_f32_16x16x4_f32 (fp32 in / fp32 accumulate). Lane l holds
+// A[l & 15][k = l >> 4], B[k = l >> 4][l & 15], C[(l >> 4) * 4 + reg][l & 15].
+// Each wave owns 16-column tiles of the output and keeps that tile's whole
+// B column (inner dimension <= 256 -> 64 registers) in registers while it
+// walks the row tiles, so M_r is read from L2 once per GEMM per positive.
+//
+// The update pass is the shared destination-major kernel in its
+// materialised mode (gradient rows summed in code order); rel_proj is
+// updated by transr_proj_apply.
+#include "kge_step_impl.h"
+
+namespace kge {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+constexpr int kTrQ = (kTrMaxSlots + kTrWaves - 1) / kTrWaves;   // slots per wave
+constexpr int kTrKV = kTrMaxDim / KGE_WAVE;                     // projected-row floats per lane
+constexpr int kTrKS = kTrMaxDim / 4;                            // MFMA k-steps held in registers
+constexpr int kTrKS3 = (kTrMaxSlots + 1 + 3) / 4;               // GEMM3 k-steps (K + 2 slot rows)
+
+// element gradient of the score wrt a = x - y (Lp kinds): score_grad's rule
+template <int SK>
+__device__ __forceinline__ float lp_elem_grad(float a, float alpha, float M) {
+  if (SK == SK_P2) return alpha * a;
+  float s = a > 0.f ? alpha : (a < 0.f ? -alpha : 0.f);
+  if (SK == SK_PINF && fabsf(a) != M) s = 0.f;
+  return s;
+}
+
+template <int SK>
+__global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  __shared__ float s_w[kTrWaves][4];
+  __shared__ int s_last;
+  const int d = T.d, k = T.k, K = A.Keff, NR = K + 2, NS = 2 * K + 4;
+  const TrLds L = tr_lds(d, k, K);
+  const int LX = L.LX, LP = L.LP, D4 = LX - 1, K4 = LP - 1;
+  float* X = sm;
+  float* P = sm + L.NR16 * LX;
+  float* S = sm;   // over X and P once both are consumed
+  float* pn = sm + L.pn;
+  float* xx = sm + L.xx;
+  float* xh = sm + L.xh;
+  float* xt = sm + L.xt;
+  float* sS = sm + L.sS;
+  float* sR = sm + L.sR;
+  float* sT = sm + L.sT;
+  float* sA = sm + L.sA;
+  float* rp = sm + L.rp;
+  int32_t* ids = reinterpret_cast<int32_t*>(sm + L.ids);
+  float* misc = sm + L.misc;
+
+  const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const int64_t i = blockIdx.x;
+  int err = 0;
+  int64_t ph = load_idx(A.pos, i * 3 + 0, A.i64);
+  int64_t pr = load_idx(A.pos, i * 3 + 1, A.i64);
+  int64_t pt = load_idx(A.pos, i * 3 + 2, A.i64);
+  if (ph < 0 || ph >= A.ent.rows) { err = KGE_ERANGE; ph = 0; }
+  if (pr < 0 || pr >= A.rel.rows) { err = KGE_ERANGE; pr = 0; }
+  if (pt < 0 || pt >= A.ent.rows) { err = KGE_ERANGE; pt = 0; }
+  for (int j = tid; j < K; j += kTrThreads) ids[j] = slot_entity(A, i, j, &err);
+  __syncthreads();
+  auto row_id = [&](int q) -> int64_t { return q == 0 ? ph : q == 1 ? pt : (int64_t)ids[q - 2]; };
+
+  // ---- gather X (pad rows and columns zero)
+  for (int row = wv; row < L.NR16; row += kTrWaves) {
+    const float* src = row < NR ? A.ent.row(row_id(row)) : nullptr;
+    for (int c = lane; c < D4; c += KGE_WAVE) X[row * LX + c] = (src && c < d) ? src[c] : 0.f;
+  }
+  __syncthreads();
+  // row statistics for the rel_proj slice norms: ||x||^2, x.h, x.t
+  for (int row = wv; row < NR; row += kTrWaves) {
+    float a = 0.f, b = 0.f, c2 = 0.f;
+    for (int c = lane; c < d; c += KGE_WAVE) {
+      const float x = X[row * LX + c];
+      a += x * x;
+      b += X[c] * x;
+      c2 += X[LX + c] * x;
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    c2 = wave_sum(c2);
+    if (lane == 0) { xx[row] = a; xh[row] = b; xt[row] = c2; }
+  }
+
+  // ---- GEMM1: P = X M_r
+  const float* Mr = T.proj.row(pr);
+  {
+    const int nct = (k + 15) / 16, nks = D4 / 4;
+    for (int ct = wv; ct < nct; ct += kTrWaves) {
+      const int col = ct * 16 + (lane & 15);
+      float bf[kTrKS];
+#pragma unroll
+      for (int ks = 0; ks < kTrKS; ++ks) {
+        const int kk = ks * 4 + (lane >> 4);
+        bf[ks] = (ks < nks && kk < d && col < k) ? Mr[(int64_t)kk * k + col] : 0.f;
+      }
+      for (int rt = 0; rt < L.NR16 / 16; ++rt) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        const float* xa = X + (rt * 16 + (lane & 15)) * LX + (lane >> 4);
+#pragma unroll
+        for (int ks = 0; ks < kTrKS; ++ks)
+          if (ks < nks) acc = mfma16(xa[ks * 4], bf[ks], acc);
+        if (col < K4) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) P[(rt * 16 + (lane >> 4) * 4 + g) * LP + col] = acc[g];
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- clip the projected rows (TransR.py:187-189, constraint.py:94-99)
+  for (int row = wv; row < NR; row += kTrWaves) {
+    float s2 = 0.f;
+    for (int c = lane; c < k; c += KGE_WAVE) s2 += P[row * LP + c] * P[row * LP + c];
+    const float n = sqrtf(wave_sum(s2));
+    if (lane == 0) pn[row] = n;
+    if (T.clip && !(n < 1.f)) {
+      const float dv = fmaxf(n, 1e-9f);
+      for (int c = lane; c < k; c += KGE_WAVE) P[row * LP + c] = P[row * LP + c] / dv;
+    }
+  }
+  __syncthreads();
+
+  // relation row r on the lanes (element c = lane + 64 v)
+  float rr[kTrKV];
+#pragma unroll
+  for (int v = 0; v < kTrKV; ++v) {
+    const int c = lane + KGE_WAVE * v;
+    rr[v] = c < k ? A.rel.row(pr)[c] : 0.f;
+  }
+  // slot q (q < K: negative q; q == K: the positive) -> x / y rows of P
+  auto xrow_of = [&](int q, int kind) { return kind == KIND_HC ? 2 + q : 0; };
+  auto yrow_of = [&](int q, int kind) { return kind == KIND_TC ? 2 + q : 1; };
+  auto kind_of = [&](int q) { return q == K ? KIND_POS : slot_kind(A.side_mode, q); };
+
+  // ---- scores: s(x, y), x = P[xrow] + r, y = P[yrow]
+  for (int m = 0; m < kTrQ; ++m) {
+    const int q = wv + kTrWaves * m;
+    if (q > K) break;
+    const int kind = kind_of(q);
+    const float* xp = P + xrow_of(q, kind) * LP;
+    const float* yp = P + yrow_of(q, kind) * LP;
+    float part = 0.f;
+    float av[kTrKV];
+#pragma unroll
+    for (int v = 0; v < kTrKV; ++v) {
+      const int c = lane + KGE_WAVE * v;
+      av[v] = 0.f;
+      if (c < k) {
+        const float x = xp[c] + rr[v], y = yp[c];
+        if (SK == SK_DOT) {
+          part += x * y;
+        } else {
+          const float a = x - y, ma = fabsf(a);
+          av[v] = a;
+          part = SK == SK_P2 ? part + ma * ma : SK == SK_P1 ? part + ma : fmaxf(part, ma);
+        }
+      }
+    }
+    const float R = SK == SK_PINF ? wave_max(part) : wave_sum(part);
+    float ties = 1.f;
+    if (SK == SK_PINF) {
+      float tq = 0.f;
+#pragma unroll
+      for (int v = 0; v < kTrKV; ++v)
+        if (lane + KGE_WAVE * v < k && fabsf(av[v]) == R) tq += 1.f;
+      ties = wave_sum(tq);
+    }
+    float lp;
+    const float s = score_value<SK>(R, A.pw, &lp);
+    if (lane == 0) { sS[q] = s; sR[q] = R; sT[q] = ties; }
+  }
+  __syncthreads();
+
+  // ---- loss and dL/ds per triple (one wave, IEEE transcendentals; every
+  // weight decided once -- the backward below reuses it)
+  if (wv == 0) {
+    const float sp = sS[K];
+    const bool sans = A.loss_kind == KGE_LOSS_SANS;
+    float Ms = -INFINITY;
+    if (sans)
+      for (int q = lane; q < K; q += KGE_WAVE) Ms = fmaxf(Ms, A.temperature * sS[q]);
+    Ms = wave_max(Ms);
+    float Z = 0.f;
+    if (sans)
+      for (int q = lane; q < K; q += KGE_WAVE) Z += expf(A.temperature * sS[q] - Ms);
+    Z = wave_sum(Z);
+    const float invZ = sans ? (Z > 0.f ? 1.f / Z : 0.f) : 1.f;
+    float lneg = 0.f, csum = 0.f;
+    for (int q = lane; q < K; q += KGE_WAVE) {
+      const float s = sS[q];
+      float lp;
+      score_value<SK>(sR[q], A.pw, &lp);
+      const float c = neg_coef(A, s, sp, Ms, invZ);
+      sA[q] = score_alpha<SK>(c, sR[q], lp, sT[q], A.pw);
+      csum += c;
+      switch (A.loss_kind) {
+        case KGE_LOSS_HINGE: lneg += fmaxf(A.margin + s - sp, 0.f); break;
+        case KGE_LOSS_LOGISTIC: lneg += logf(1.f + expf(s - sp)); break;
+        case KGE_LOSS_BCE: lneg += log_sigmoid(-s); break;
+        case KGE_LOSS_SANS: lneg += expf(A.temperature * s - Ms) * invZ * log_sigmoid(-s - A.margin); break;
+        default: lneg += s * s; break;
+      }
+    }
+    lneg = wave_sum(lneg);
+    csum = wave_sum(csum);
+    if (lane == 0) {
+      float lossp, cp;
+      switch (A.loss_kind) {
+        case KGE_LOSS_HINGE: lossp = lneg * A.inv_bk; cp = -csum; if (K == 0) lossp = NAN; break;
+        case KGE_LOSS_LOGISTIC: lossp = lneg; cp = -csum; break;
+        case KGE_LOSS_BCE: lossp = -(log_sigmoid(sp) + lneg) * A.inv_b; cp = -sigmoid(-sp) * A.inv_b; break;
+        case KGE_LOSS_SANS:
+          lossp = -(log_sigmoid(sp + A.margin) + lneg) * A.inv_b;
+          cp = -sigmoid(-(sp + A.margin)) * A.inv_b;
+          break;
+        default: lossp = ((sp - 1.f) * (sp - 1.f) + lneg) * 0.5f * A.inv_b; cp = (sp - 1.f) * A.inv_b; break;
+      }
+      float lpp;
+      score_value<SK>(sR[K], A.pw, &lpp);
+      sA[K] = score_alpha<SK>(cp, sR[K], lpp, sT[K], A.pw);
+      misc[0] = lossp;
+      if (A.pos_score_out) A.pos_score_out[i] = sp;
+    }
+  }
+  if (A.neg_score_out)
+    for (int q = tid; q < K; q += kTrThreads) A.neg_score_out[i * K + q] = sS[q];
+  __syncthreads();
+
+  float n_ent = 0.f, n_rel = 0.f, n_proj = 0.f;
+  if (A.train) {
+    // ---- per-triple gradients wrt the projected rows, back through the clip;
+    // kept in registers until every wave has finished reading P
+    float G[kTrQ][2][kTrKV];   // [slot][0: positive side (h for pos), 1: entity side (t for pos)]
+    float rsum[kTrKV];
+#pragma unroll
+    for (int v = 0; v < kTrKV; ++v) rsum[v] = 0.f;
+#pragma unroll
+    for (int m = 0; m < kTrQ; ++m) {
+      const int q = wv + kTrWaves * m;
+      if (q > K) break;
+      const int kind = kind_of(q);
+      const int xr = xrow_of(q, kind), yr = yrow_of(q, kind);
+      const float* xp = P + xr * LP;
+      const float* yp = P + yr * LP;
+      const float alpha = sA[q], Mx = sR[q];
+      float gx[kTrKV], gy[kTrKV];
+      float gxx = 0.f, dx = 0.f, dy = 0.f;
+#pragma unroll
+      for (int v = 0; v < kTrKV; ++v) {
+        const int c = lane + KGE_WAVE * v;
+        gx[v] = gy[v] = 0.f;
+        if (c < k) {
+          const float x = xp[c] + rr[v], y = yp[c];
+          if (SK == SK_DOT) {
+            gx[v] = alpha * y;
+            gy[v] = alpha * x;
+          } else {
+            gx[v] = lp_elem_grad<SK>(x - y, alpha, Mx);
+            gy[v] = -gx[v];
+          }
+          gxx += gx[v] * gx[v];
+          rsum[v] += gx[v];               // the r-lookup slice is d s / d x
+          dx += gx[v] * xp[c];
+          dy += gy[v] * yp[c];
+        }
+      }
+      n_rel += gxx;
+      dx = wave_sum(dx);
+      dy = wave_sum(dy);
+      // through clip_constraint: rows with norm >= 1 were divided by it
+      const float nx = pn[xr], ny = pn[yr];
+      const bool cx = T.clip && !(nx < 1.f), cy = T.clip && !(ny < 1.f);
+      float a2 = 0.f, b2 = 0.f, ab = 0.f;
+#pragma unroll
+      for (int v = 0; v < kTrKV; ++v) {
+        const int c = lane + KGE_WAVE * v;
+        if (c < k) {
+          if (cx) gx[v] = (gx[v] - dx * xp[c]) / nx;
+          if (cy) gy[v] = (gy[v] - dy * yp[c]) / ny;
+        }
+        a2 += gx[v] * gx[v];
+        b2 += gy[v] * gy[v];
+        ab += gx[v] * gy[v];
+      }
+      a2 = wave_sum(a2);
+      b2 = wave_sum(b2);
+      ab = wave_sum(ab);
+      // rel_proj slice of this triple: x_h (x) g_h + x_t (x) g_t
+      const float hx = xx[xr], tx = xx[yr];
+      const float htx = kind == KIND_POS ? xh[1] : (kind == KIND_TC ? xh[2 + q] : xt[2 + q]);
+      n_proj += hx * a2 + tx * b2 + 2.f * htx * ab;
+      // x side is the head's projection, y side the tail's
+#pragma unroll
+      for (int v = 0; v < kTrKV; ++v) {
+        if (kind == KIND_HC) { G[m][0][v] = gy[v]; G[m][1][v] = gx[v]; }
+        else { G[m][0][v] = gx[v]; G[m][1][v] = gy[v]; }
+      }
+    }
+    __syncthreads();   // P is dead from here: S overwrites X and P
+    // S rows: [0] sum of h-slices, [1] sum of t-slices, [2 + q] negative q's
+    // entity slice, [K + 2] / [K + 3] the positive's h / t slices, [K + 4 + q]
+    // negative q's positive-side slice; rows to SR16 zero
+#pragma unroll
+    for (int m = 0; m < kTrQ; ++m) {
+      const int q = wv + kTrWaves * m;
+      if (q > K) break;
+      const int r0 = q == K ? K + 2 : K + 4 + q;   // positive-side slice
+      const int r1 = q == K ? K + 3 : 2 + q;       // entity side (the positive's t)
+#pragma unroll
+      for (int v = 0; v < kTrKV; ++v) {
+        const int c = lane + KGE_WAVE * v;
+        if (c < K4) {
+          S[r0 * LP + c] = G[m][0][v];
+          S[r1 * LP + c] = G[m][1][v];
+        }
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < kTrKV; ++v) {
+      const int c = lane + KGE_WAVE * v;
+      if (c < K4) rp[wv * LP + c] = rsum[v];
+    }
+    for (int e = tid; e < (L.SR16 - NS) * LP; e += kTrThreads) S[NS * LP + e] = 0.f;
+    __syncthreads();
+    // summed positive rows, in slot order (deterministic): h = pos + tc slices,
+    // t = pos + hc slices; r = the waves' partial sums in wave order
+    float* gp = A.gpos + i * 3 * (int64_t)A.gcols;
+    for (int c = tid; c < K4; c += kTrThreads) {
+      float h = S[(K + 2) * LP + c], t = S[(K + 3) * LP + c];
+      for (int q = 0; q < K; ++q) {
+        const float v = S[(K + 4 + q) * LP + c];
+        if (slot_kind(A.side_mode, q) == KIND_TC) h += v; else t += v;
+      }
+      S[c] = h;
+      S[LP + c] = t;
+      float r = 0.f;
+      for (int w = 0; w < kTrWaves; ++w) r += rp[w * LP + c];
+      if (c < k) gp[A.gcols + c] = r;
+    }
+    __syncthreads();
+
+    // ---- GEMM2: Y = S M_r^T -> entity-row gradients and slice norms
+    {
+      const int nct = (d + 15) / 16, nks = K4 / 4, nrt = (NS + 15) / 16;
+      for (int ct = wv; ct < nct; ct += kTrWaves) {
+        const int col = ct * 16 + (lane & 15);
+        float bf[kTrKS];
+#pragma unroll
+        for (int ks = 0; ks < kTrKS; ++ks) {
+          const int kk = ks * 4 + (lane >> 4);
+          bf[ks] = (ks < nks && kk < k && col < d) ? Mr[(int64_t)col * k + kk] : 0.f;
+        }
+        for (int rt = 0; rt < nrt; ++rt) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          const float* sa = S + (rt * 16 + (lane & 15)) * LP + (lane >> 4);
+#pragma unroll
+          for (int ks = 0; ks < kTrKS; ++ks)
+            if (ks < nks) acc = mfma16(sa[ks * 4], bf[ks], acc);
+          if (col < d) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int row = rt * 16 + (lane >> 4) * 4 + g;
+              const float v = acc[g];
+              if (row == 0) gp[col] = v;
+              else if (row == 1) gp[2 * A.gcols + col] = v;
+              else if (row < NS) {
+                n_ent += v * v;
+                if (row < NR) A.gneg[(int64_t)(((uint32_t)i << A.kshift) | (uint32_t)(row - 2)) * d + col] = v;
+              }
+            }
+          }
+        }
+      }
+    }
+    // ---- GEMM3: dM_i = X^T S[0 .. K+2) (X re-read from the table: L2)
+    {
+      const int nrt = (d + 15) / 16, nct = (k + 15) / 16, nks = (NR + 3) / 4;
+      float* dm = T.dmpart + i * (int64_t)d * k;
+      for (int rt = wv; rt < nrt; rt += kTrWaves) {
+        const int ci = rt * 16 + (lane & 15);
+        float af[kTrKS3];
+#pragma unroll
+        for (int ks = 0; ks < kTrKS3; ++ks) {
+          const int kk = ks * 4 + (lane >> 4);
+          af[ks] = (ks < nks && kk < NR && ci < d) ? A.ent.row(row_id(kk))[ci] : 0.f;
+        }
+        for (int ct = 0; ct < nct; ++ct) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          const float* sb = S + (lane >> 4) * LP + ct * 16 + (lane & 15);
+#pragma unroll
+          for (int ks = 0; ks < kTrKS3; ++ks)
+            if (ks < nks) acc = mfma16(af[ks], sb[ks * 4 * LP], acc);
+          const int col = ct * 16 + (lane & 15);
+          if (col < k) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int row = rt * 16 + (lane >> 4) * 4 + g;
+              if (row < d) dm[(int64_t)row * k + col] = acc[g];
+            }
+          }
+        }
+      }
+    }
+    // ---- destination keys for the update pass
+    for (int q = tid; q < K; q += kTrThreads) bin_key(A, ids[q], ((uint32_t)i << A.kshift) | (uint32_t)q);
+    if (tid < 3) {
+      const int64_t dest = tid == 0 ? ph : tid == 1 ? pt : A.ent.rows + pr;
+      bin_key(A, dest, A.nkeyneg + ((uint32_t)i << 2) + (uint32_t)tid);
+    }
+  }
+  if (err) set_status(A.status, err);
+
+  // ---- partials: loss, ||g||^2 per variable (0 ent, 1 rel_emb, 2 rel_proj);
+  // the last workgroup reduces them in a fixed order
+  n_ent = wave_sum(n_ent);
+  n_rel = wave_sum(n_rel);
+  if (lane == 0) { s_w[wv][0] = n_ent; s_w[wv][1] = n_rel; s_w[wv][2] = n_proj; }
+  __syncthreads();
+  if (tid == 0) {
+    float acc[5] = {misc[0], 0.f, 0.f, 0.f, 0.f};
+    for (int w = 0; w < kTrWaves; ++w) {
+      acc[1] += s_w[w][0];
+      acc[2] += s_w[w][1];
+      acc[3] += s_w[w][2];
+    }
+#pragma unroll
+    for (int c = 0; c < 5; ++c)
+      __hip_atomic_store(&A.part[(int64_t)blockIdx.x * 8 + c], acc[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0);
+    const uint32_t prev = __hip_atomic_fetch_add(&A.ctl->score_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (uint32_t)(gridDim.x - 1);
+  }
+  __syncthreads();
+  if (s_last && wv == 0) {
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int w = lane; w < (int)gridDim.x; w += KGE_WAVE) {
+#pragma unroll
+      for (int c = 0; c < 5; ++c)
+        acc[c] += __hip_atomic_load(&A.part[(int64_t)w * 8 + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int c = 0; c < 5; ++c) acc[c] = wave_sum(acc[c]);
+    if (lane == 0) {
+      A.loss_out[0] = acc[0];
+      if (A.loss_accum) A.loss_accum[0] += acc[0];
+      A.ctl->loss = acc[0];
+      A.ctl->score_ticket = 0u;
+      A.ctl->ovf_len = __hip_atomic_exchange(&A.ctl->ovf_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        A.ctl->scale[v] = -A.lr * (A.clip_norm / fmaxf(sqrtf(acc[1 + v]), A.clip_norm));
+        if (A.norm2_out) A.norm2_out[v] = acc[1 + v];
+      }
+    }
+  }
+}
+
+// rel_proj update: per relation, the positives' dM partials summed in
+// sorted (positive) order, clip scale, SGD -- or the dense gradient in
+// KGE_OPT_GRAD mode. 1024 elements of M_r per workgroup.
+__global__ __launch_bounds__(256) void transr_proj_apply(StepArgs A, TrArgs T) {
+  const int64_t dk = (int64_t)T.d * T.k;
+  const int64_t chunks = (dk + 1023) / 1024;
+  const int64_t r = blockIdx.x / chunks, ch = blockIdx.x % chunks;
+  const int64_t beg = rel_lower(T.srel, 0, A.B, r), end = rel_lower(T.srel, beg, A.B, r + 1);
+  if (beg == end) return;
+  const float sc = A.ctl->scale[2];
+  const int64_t e1 = min(dk, (ch + 1) * 1024);
+  for (int64_t e = ch * 1024 + threadIdx.x; e < e1; e += 256) {
+    float g = 0.f;
+    for (int64_t p = beg; p < end; ++p) g += T.dmpart[(int64_t)T.sorted[p] * dk + e];
+    if (T.gproj_out) T.gproj_out[r * dk + e] = g;
+    else {
+      float* w = T.proj.p + r * T.proj.ld + e;
+      *w = *w + g * sc;
+    }
+  }
+}
+
+static void launch_update_mat(const StepArgs& A, const StepGeom& G, hipStream_t st) {
+#define KGE_UPD(V, N) \
+  hipLaunchKernelGGL((update_kernel<Materialised, V, N, SK_DOT>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A)
+  if (G.vec == 4) {
+    if (G.nc == 1) KGE_UPD(4, 1); else if (G.nc == 2) KGE_UPD(4, 2); else KGE_UPD(4, 4);
+  } else {
+    if (G.nc == 1) KGE_UPD(1, 1); else if (G.nc == 2) KGE_UPD(1, 2); else KGE_UPD(1, 4);
+  }
+#undef KGE_UPD
+}
+
+template <int SK>
+static void launch_tr(const StepArgs& A, const StepGeom& G, const TrArgs& T, const RelArgs& P, hipStream_t st,
+                      hipEvent_t const* ev) {
+  if (A.train) launch_rel_rank(P, st);
+  const TrLds L = tr_lds(T.d, T.k, A.Keff);
+  hipLaunchKernelGGL(transr_kernel<SK>, dim3((unsigned)A.B), dim3(kTrThreads), (size_t)L.total_floats * 4, st, A, T);
+  if (ev) (void)hipEventRecord(ev[2], st);
+  if (A.train) {
+    launch_update_mat(A, G, st);
+    const int64_t chunks = ((int64_t)T.d * T.k + 1023) / 1024;
+    hipLaunchKernelGGL(transr_proj_apply, dim3((unsigned)(T.proj.rows * chunks)), dim3(256), 0, st, A, T);
+  }
+}
+
+kge_status launch_step_transr(const StepArgs& A, const StepGeom& G, const TrArgs& T, const RelArgs& P, int sk,
+                              hipStream_t st, hipEvent_t const* ev) {
+  switch (sk) {
+    case SK_P1: launch_tr<SK_P1>(A, G, T, P, st, ev); break;
+    case SK_P2: launch_tr<SK_P2>(A, G, T, P, st, ev); break;
+    case SK_PINF: launch_tr<SK_PINF>(A, G, T, P, st, ev); break;
+    default: launch_tr<SK_DOT>(A, G, T, P, st, ev); break;
+  }
+  return KGE_OK;
+}
+
+}  // namespace kge

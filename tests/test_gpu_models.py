@@ -83,3 +83,34 @@ def test_step_golden_fused(meta):
     assert abs(float(step.loss_out) - float(z[tag + "/loss"])) <= 1e-5 * max(1.0, abs(float(z[tag + "/loss"])))
     for k in W:
         np.testing.assert_allclose(m.model_weights[k].cpu().numpy(), z["%s/out/%s" % (tag, k)], atol=1e-5, err_msg=k)
+
+
+def test_unsupported_plans_take_plugin_path():
+    """Combinations the library has no instance for (kge_step_workspace_bytes
+    == 0) go to the eager plugin path instead of raising: RotatE rows of 2000
+    floats (d = 1000), RESCAL without its regulariser."""
+    from KGE import engine, loss, optimizers, score
+    from KGE.models.semantic_based.RESCAL import RESCAL
+    from KGE.models.translating_based.RotatE import RotatE
+    from KGE.ns_strategy import UniformStrategy
+    dev = torch.device("cuda", 0)
+    E, R = 30, 4
+    md = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
+    m = RotatE({"embedding_size": 1000}, 2, "h+t", score_fn=score.LpDistance(1),
+               loss_fn=loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
+               ns_strategy=UniformStrategy(np.arange(E), seed=1))
+    m.metadata = md
+    m.model_weights = {"ent_emb": torch.rand(E, 1000, 2, device=dev), "rel_emb": torch.rand(R, 1000, device=dev)}
+    assert "exceeds" in engine.fused_plan(m, optimizers.SGD(0.01))
+    m2 = RESCAL({"embedding_size": 8}, 2, "h+t", loss_fn=loss.SquareErrorLoss(), constraint=False,
+                ns_strategy=UniformStrategy(np.arange(E), seed=1))
+    m2.metadata = md
+    m2.model_weights = {"ent_emb": torch.rand(E, 8, device=dev), "rel_inter": torch.rand(R, 8, 8, device=dev)}
+    assert "constraint" in engine.fused_plan(m2, optimizers.SGD(0.01))
+    X = np.stack([np.arange(8) % E, np.arange(8) % R, (np.arange(8) * 7) % E], 1)
+    for mm in (m, m2):
+        mm.model_weights = {k: v.cpu() for k, v in mm.model_weights.items()}
+        with pytest.warns(UserWarning, match="eager plugin path"):
+            mm.train(train_X=X, val_X=X, metadata=md, epochs=1, batch_size=4, optimizer="SGD",
+                     seed=1, model_weights_initial=None)
+        assert np.isfinite(mm.train_loss_history[0])

@@ -25,16 +25,20 @@ def _dev():
     return torch.device("cuda", 0)
 
 
-def _make(model_name, d, K, side, score_fn, loss_fn, E, R, sampler, constraint=True):
+def _make(model_name, d, K, side, score_fn, loss_fn, E, R, sampler, constraint=True, k=None):
     from KGE.models.semantic_based.DistMult import DistMult
     from KGE.models.semantic_based.RESCAL import RESCAL
     from KGE.models.translating_based.RotatE import RotatE
     from KGE.models.translating_based.TransE import TransE
+    from KGE.models.translating_based.TransR import TransR
     common = dict(loss_fn=loss_fn, ns_strategy=sampler)
     if model_name == "TransE":
         m = TransE({"embedding_size": d}, K, side, score_fn=score_fn, constraint=constraint, **common)
     elif model_name == "RotatE":
         m = RotatE({"embedding_size": d}, K, side, score_fn=score_fn, **common)
+    elif model_name == "TransR":
+        m = TransR({"ent_embedding_size": d, "rel_embedding_size": k or d}, K, side, score_fn=score_fn,
+                   constraint=constraint, **common)
     elif model_name == "RESCAL":
         m = RESCAL({"embedding_size": d}, K, side, constraint=constraint, constraint_weight=0.5, **common)
     else:
@@ -43,10 +47,15 @@ def _make(model_name, d, K, side, score_fn, loss_fn, E, R, sampler, constraint=T
     return m
 
 
-def _weights(model_name, E, R, d, rng):
+def _weights(model_name, E, R, d, rng, k=None):
     if model_name == "RotatE":
         return {"ent_emb": rng.uniform(-0.5, 0.5, (E, d, 2)).astype(np.float32),
                 "rel_emb": rng.uniform(-0.5, 0.5, (R, d)).astype(np.float32)}
+    if model_name == "TransR":
+        k = k or d
+        return {"ent_emb": rng.uniform(-0.5, 0.5, (E, d)).astype(np.float32),
+                "rel_emb": rng.uniform(-0.5, 0.5, (R, k)).astype(np.float32),
+                "rel_proj": (np.eye(d, k)[None] + rng.uniform(-0.2, 0.2, (R, d, k))).astype(np.float32)}
     if model_name == "RESCAL":
         return {"ent_emb": rng.uniform(-0.5, 0.5, (E, d)).astype(np.float32),
                 "rel_inter": rng.uniform(-0.2, 0.2, (R, d, d)).astype(np.float32)}
@@ -77,18 +86,18 @@ def _spec_loss(lf):
 
 
 def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, idx=torch.int64, train=True,
-             seed=11, constraint=True, typed=None, lr=0.05, opt="sgd", flags=0):
+             seed=11, constraint=True, typed=None, lr=0.05, opt="sgd", flags=0, k=None):
     from KGE import engine, optimizers
     from KGE.ns_strategy import TypedStrategy, UniformStrategy
     dev = _dev()
     rng = np.random.default_rng(seed)
-    W = _weights(model_name, E, R, d, rng)
+    W = _weights(model_name, E, R, d, rng, k)
     pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
     if typed is None:
         sampler = UniformStrategy(np.arange(E), seed=seed)
     else:
         sampler = TypedStrategy(None, {"ind2type": typed}, seed=seed)
-    m = _make(model_name, d, K, side, score_fn, loss_fn, E, R, sampler, constraint)
+    m = _make(model_name, d, K, side, score_fn, loss_fn, E, R, sampler, constraint, k)
     m.model_weights = {k: torch.tensor(v, device=dev) for k, v in W.items()}
     step = engine.FusedStep(m)
     step.flags = flags
@@ -199,6 +208,36 @@ def test_rescal_validation_and_adam(hiplib):
                                           train=False)
     check(ref, got, l_, ps, ns)
     ref, got, l_, ps, ns, _, _ = run_case(hiplib, "RESCAL", 32, 12, 4, "h+t", None,
+                                          loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), opt="adam", lr=0.01)
+    check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("si", [0, 1, 2, 3, 5])
+@pytest.mark.parametrize("li", [0, 3, 4])
+def test_transr(hiplib, si, li):
+    """TransR (three per-positive MFMA products + clip) vs the oracle: every
+    score kind x hinge / SANS / square error; d != k; some rows clipped."""
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransR", 24, 10, 6, "h+t", _scores()[si], _losses()[li], k=20)
+    check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("d,k,B,K,side,constraint", [(200, 200, 6, 64, "h+t", True), (32, 48, 17, 3, "t", True),
+                                                      (40, 16, 9, 5, "h", False), (17, 33, 5, 70, "h+t", True)])
+def test_transr_shapes(hiplib, d, k, B, K, side, constraint):
+    """C4's TransR shape (d = k = 200, K = 64) at reduced batch; odd sizes;
+    the constraint off (no clip, no table assigns)."""
+    from KGE import loss, score
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransR", d, B, K, side, score.LpDistancePow(2),
+                                          loss.PairwiseHingeLoss(1.0), k=k, constraint=constraint, E=90, R=4)
+    check(ref, got, l_, ps, ns)
+
+
+def test_transr_validation_and_adam(hiplib):
+    from KGE import loss, score
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransR", 32, 12, 4, "h+t", score.LpDistancePow(2),
+                                          loss.PairwiseHingeLoss(1.0), train=False)
+    check(ref, got, l_, ps, ns)
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransR", 32, 12, 4, "h+t", score.LpDistance(2),
                                           loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), opt="adam", lr=0.01)
     check(ref, got, l_, ps, ns)
 
