@@ -48,6 +48,7 @@ struct Plan {
   // dense-gradient / relation-matrix models (RESCAL)
   uint64_t o_upart, o_sorted, o_srel, o_gproj, o_rpart, o_regpart, o_gent, o_grel;
   uint64_t o_gneg, o_dm;   // TransR
+  uint64_t o_touched;
   bool rescal, transr;
 };
 
@@ -204,7 +205,16 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.G.vec = vec;
   P.G.nc = ncp;
   P.G.nWG = (int)nWG;
-  P.G.gridU = (int)ceil_div(ndest, kUpdWaves);
+  // compact update launch: when the tables have far more rows than the step
+  // has keys, visit only the touched destinations (not with a fused full-table
+  // constraint or a dense gradient, which rewrite every row)
+  const bool fuse_norm_plan = d->optimizer == KGE_OPT_SGD && d->constraint &&
+                              !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT) &&
+                              (model == KGE_MODEL_TRANSE || model == KGE_MODEL_DISTMULT) &&
+                              !(d->flags & KGE_FLAG_DEBUG_UNFUSED_CONSTRAINT);
+  const bool compact = !rescal && !fuse_norm_plan && ndest > 2 * T;
+  const int64_t nupd = compact ? T : ndest;
+  P.G.gridU = (int)ceil_div(nupd, kUpdWaves);
   P.rescal = rescal;
   P.transr = transr;
   P.G.lds_score = (size_t)SL.total;
@@ -221,9 +231,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   // every entity row is renormalised by the step itself: rows on the stream
   // as they are loaded, every row again (bit-identically) by the update
   // kernel, which writes the normalised row plus this step's SGD delta
-  A.fuse_norm = d->optimizer == KGE_OPT_SGD && d->constraint && !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT) &&
-                (model == KGE_MODEL_TRANSE || model == KGE_MODEL_DISTMULT) &&
-                !(d->flags & KGE_FLAG_DEBUG_UNFUSED_CONSTRAINT);
+  A.fuse_norm = fuse_norm_plan;
+  A.compact = compact;
   A.gent = d->grad_out[0];
   A.grel = d->grad_out[1];
   A.given = sm.kind == KGE_SAMPLER_GIVEN;
@@ -279,6 +288,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.o_list = take((uint64_t)ndest * cap * 4);
   P.o_ovf = take((uint64_t)T * 8);
   P.o_upart = take((uint64_t)P.G.gridU * 4);
+  P.o_touched = take((uint64_t)(compact ? T : 1) * 4);
   if (rescal) {
     const int64_t nct = ceil_div(d->dim, 16);
     P.o_sorted = take((uint64_t)B * 4);
@@ -407,6 +417,7 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   A.list = (uint32_t*)(ws + P.o_list);
   A.ovf = (uint64_t*)(ws + P.o_ovf);
   A.upart = (float*)(ws + P.o_upart);
+  A.touched = (uint32_t*)(ws + P.o_touched);
   A.gpe = A.gpos;
   A.gpe_stride = 3 * A.gcols;
   A.gpe_toff = 2 * A.gcols;

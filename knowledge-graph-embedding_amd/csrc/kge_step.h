@@ -24,8 +24,10 @@ struct StepCtl {
   float loss;
   uint32_t rel_ticket;     // relation-matrix gradient workgroups done (rel norm^2)
   uint32_t reg_ticket;     // regulariser-loss workgroups done
-  uint32_t pad0;
+  uint32_t ntouched;       // compact mode: destinations filed so far by the running score kernel
   float dn2[4];            // norm^2 of the dense (duplicate-summed) gradient per variable
+  uint32_t touched_len;    // compact mode: destinations for the update kernel (set by the last score workgroup)
+  uint32_t pad1[3];
 };
 
 // Everything a step kernel needs, passed by value (kernarg segment).
@@ -64,6 +66,11 @@ struct StepArgs {
   int32_t gpe_stride, gpe_toff;
   float* upart;     // [gridU] update-kernel norm^2 partials (dense mode)
   float* gneg;      // materialised family: [B << kshift, ent.cols] negatives' entity-row gradients
+  // compact update launch (tables much larger than a step's keys): the score
+  // pass appends each destination's first key to `touched`, and the update
+  // kernel visits only those rows (untouched rows are not read or written)
+  bool compact;
+  uint32_t* touched;
   // geometry
   int32_t wpp;      // waves per positive (1, 2, 4, 8)
   int32_t nP;       // positives per score workgroup = kStepWaves / wpp

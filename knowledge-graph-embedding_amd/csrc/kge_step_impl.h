@@ -119,6 +119,7 @@ __device__ __forceinline__ float neg_coef(const StepArgs& A, float s, float sp, 
 // order), or to the overflow list once that list is full
 __device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_t code) {
   const uint32_t r = atomicAdd(&A.cnt[dest], 1u);
+  if (A.compact && r == 0u) A.touched[atomicAdd(&A.ctl->ntouched, 1u)] = (uint32_t)dest;
   if (r < (uint32_t)A.cap) {
     A.list[dest * A.cap + r] = code;
   } else {
@@ -605,6 +606,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
         // every workgroup's keys are filed: hand the overflow length to the
         // update kernel and restart the overflow list for the next step
         A.ctl->ovf_len = __hip_atomic_exchange(&A.ctl->ovf_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        A.ctl->touched_len = __hip_atomic_exchange(&A.ctl->ntouched, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         A.ctl->scale[tid - 1] = -A.lr * (A.clip_norm / fmaxf(sqrtf(s), A.clip_norm));
         if (A.norm2_out) A.norm2_out[tid - 1] = s;
@@ -643,7 +645,15 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
   const int64_t R_ = A.rel_dests ? A.rel.rows : 0;
   const int64_t ndest = E_ + R_;
   const int64_t dd = (int64_t)blockIdx.x * kUpdWaves + wv;
-  const int64_t d = dd < R_ ? E_ + dd : dd - R_;
+  int64_t d;
+  bool active;
+  if (A.compact) {   // only the destinations this step touched
+    active = dd < (int64_t)A.ctl->touched_len;
+    d = active ? (int64_t)A.touched[dd] : 0;
+  } else {
+    active = dd < ndest;
+    d = dd < R_ ? E_ + dd : dd - R_;
+  }
   const uint32_t nneg = A.nkeyneg;
   const uint32_t kmask = (1u << A.kshift) - 1u;
   const uint32_t snap_stride = (uint32_t)(M::NSNAP * A.snap_cols);   // B * stride < 2^32 (plan check)
@@ -728,7 +738,7 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
   };
 
   float dn2 = 0.f;   // dense mode: this wave's ||summed row gradient||^2
-  if (dd < ndest) {
+  if (active) {
     const bool is_ent = d < E_;
     const uint32_t* lst = A.list + d * (int64_t)A.cap;
     // issued together: the counter, the list's first 64 entries (speculative;

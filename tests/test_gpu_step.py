@@ -242,6 +242,48 @@ def test_transr_validation_and_adam(hiplib):
     check(ref, got, l_, ps, ns)
 
 
+@pytest.mark.parametrize("model_name", ["TransE", "DistMult", "RotatE", "TransR"])
+def test_compact_update_large_table(hiplib, model_name):
+    """E = 6000 rows vs 8 x (5 + 3) keys: the update kernel visits only the
+    destinations the step touched (compact launch), untouched rows unchanged."""
+    from KGE import loss, score
+    sc = None if model_name == "DistMult" else score.LpDistance(2)
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, model_name, 32, 8, 5, "h+t", sc,
+                                          loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E=6000, R=9,
+                                          constraint=False)
+    check(ref, got, l_, ps, ns)
+
+
+def test_compact_update_consecutive_steps(hiplib):
+    """Three steps through one workspace in compact mode (the touched-list
+    counter resets itself) == three oracle steps."""
+    from KGE import engine, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    dev = _dev()
+    rng = np.random.default_rng(8)
+    E, R, d, B, K = 3000, 5, 40, 11, 6
+    W = _weights("TransE", E, R, d, rng)
+    sampler = UniformStrategy(np.arange(E), seed=6)
+    m = _make("TransE", d, K, "h+t", score.LpDistance(1), loss.PairwiseHingeLoss(1.0), E, R, sampler,
+              constraint=False)
+    m.model_weights = {k: torch.tensor(v, device=dev) for k, v in W.items()}
+    step = engine.FusedStep(m)
+    opt = optimizers.SGD(0.05)
+    ref_w = W
+    for it in range(3):
+        pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+        plane = sampler.offset
+        step(torch.tensor(pos, device=dev), True, opt)
+        torch.cuda.synchronize()
+        step.check_status()
+        neg = orc.negatives(pos, K, "h+t", E, seed=6, plane=plane)
+        ref = orc.train_step("TransE", ref_w, pos, neg, score=("lp", 1.0), loss=("hinge", 1.0), lr=0.05,
+                             constraint=False)
+        ref_w = ref["weights"]
+        for k, v in ref_w.items():
+            np.testing.assert_allclose(m.model_weights[k].cpu().numpy(), v, atol=TOL, err_msg="%s step %d" % (k, it))
+
+
 def test_int32_ids_and_validation_step(hiplib):
     from KGE import loss, score
     ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransE", 32, 12, 4, "h+t", score.LpDistance(2),
