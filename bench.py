@@ -1,6 +1,6 @@
 """bench.py -- KGE training-step throughput on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): TransE, d=200,
+Default workload (BASELINE.json configs[1]): TransE, d=200,
 batch 1024 positives x 256 negatives ('h+t'), LpDistance(2),
 SelfAdversarialNegativeSamplingLoss(3, 1), uniform sampling, constraint=True
 (entity rows renormalised every step), SGD lr=0.01, on the FB15k-237 training
@@ -8,12 +8,17 @@ graph (272,115 triples, E=14,505, R=237; ids shipped in data/). One "step" =
 one call of the fused kge_step (sample -> gather -> score -> loss -> grad ->
 clip -> sparse SGD update) on a batch already resident in HBM.
 
+Other legs (``--workload``; one JSON line each, same schema):
+  c1         TransE d=50, B=128, K=1, hinge(1), corrupt_side='t' (launch-bound)
+  c3         RotatE d=256, B=1024, K=256, SANS(3,1), LpDistance(1)
+  c4-rescal  RESCAL d=200, B=512, K=64, SquareError, constraint (dense regulariser)
+  c4-transr  TransR d=k=200, B=512, K=64, LpDistancePow(2), hinge(1), constraint (fp32 MFMA)
+  c2-50m     the C2 step on a synthetic 50M-entity table (HBM-honest point; SURVEY 8(d) Caveat)
+
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 one process per GPU, each with its own 1024-positive batch (weak scaling, the
 global batch is N*1024); the entity table is row-sharded across the ranks
-(KGE/sharded.py: all-gather of the shards, fused gradient step, RCCL
-reduce-scatter of the entity gradient + all-reduce of the relation gradient,
-global clip norm and loss, sharded SGD apply).
+(KGE/sharded.py).
 
 Prints ONE JSON line (rank 0).
 """
@@ -22,6 +27,7 @@ import argparse
 import ctypes
 import json
 import os
+import platform
 import sys
 import time
 
@@ -35,7 +41,10 @@ for p in (ROOT, PKG):
 
 import torch  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+F32_MFMA_PEAK_TF = 157.3   # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+
+WORKLOADS = ("c2", "c1", "c3", "c4-rescal", "c4-transr", "c2-50m")
 
 
 def parse():
@@ -43,9 +52,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=1024)
-    ap.add_argument("--neg", type=int, default=256)
-    ap.add_argument("--dim", type=int, default=200)
+    ap.add_argument("--workload", default="c2", choices=WORKLOADS)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--neg", type=int, default=None)
+    ap.add_argument("--dim", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -56,7 +66,82 @@ def load_graph():
     return z["triples"].astype(np.int64), int(z["n_entities"]), int(z["n_relations"])
 
 
-def algorithmic_bytes(B, K, d, E):
+# ---------------------------------------------------------------- workloads
+def spec(name, args):
+    """(model ctor kwargs, B, K, d, side, E override) of a workload."""
+    from KGE import loss, score
+    w = {
+        "c2": dict(model="TransE", B=1024, K=256, d=200, side="h+t", constraint=True,
+                   score=score.LpDistance(p=2), loss=loss.SelfAdversarialNegativeSamplingLoss(margin=3, temperature=1),
+                   desc="C2: TransE d=%(d)d, batch=%(B)d, %(K)d negs h+t, SANS(3,1), LpDistance(2), uniform, "
+                        "constraint, SGD"),
+        "c1": dict(model="TransE", B=128, K=1, d=50, side="t", constraint=True, score=score.LpDistance(p=2),
+                   loss=loss.PairwiseHingeLoss(margin=1),
+                   desc="C1: TransE d=%(d)d, batch=%(B)d, %(K)d neg/pos corrupt_side='t', hinge(1), LpDistance(2), "
+                        "uniform, constraint, SGD"),
+        "c3": dict(model="RotatE", B=1024, K=256, d=256, side="h+t", constraint=False, score=score.LpDistance(p=1),
+                   loss=loss.SelfAdversarialNegativeSamplingLoss(margin=3, temperature=1),
+                   desc="C3: RotatE d=%(d)d (complex), batch=%(B)d, %(K)d negs h+t, SANS(3,1), LpDistance(1), "
+                        "uniform, SGD"),
+        "c4-rescal": dict(model="RESCAL", B=512, K=64, d=200, side="h+t", constraint=True, score=None,
+                          loss=loss.SquareErrorLoss(),
+                          desc="C4: RESCAL d=%(d)d, batch=%(B)d, %(K)d negs h+t, SquareError, constraint "
+                               "(dense Lp regulariser), uniform, SGD"),
+        "c4-transr": dict(model="TransR", B=512, K=64, d=200, side="h+t", constraint=True,
+                          score=score.LpDistancePow(p=2), loss=loss.PairwiseHingeLoss(margin=1),
+                          desc="C4: TransR d=k=%(d)d, batch=%(B)d, %(K)d negs h+t, LpDistancePow(2), hinge(1), "
+                               "constraint (clip), uniform, SGD"),
+        "c2-50m": dict(model="TransE", B=1024, K=256, d=200, side="h+t", constraint=False,
+                       score=score.LpDistance(p=2),
+                       loss=loss.SelfAdversarialNegativeSamplingLoss(margin=3, temperature=1), E=50_000_000,
+                       desc="C2 step on a synthetic %(E)d-entity table: TransE d=%(d)d, batch=%(B)d, %(K)d negs h+t, "
+                            "SANS(3,1), LpDistance(2), uniform ids, no constraint (a full-table renormalisation "
+                            "would be an 80 GB pass per step), SGD"),
+    }[name]
+    if args.batch:
+        w["B"] = args.batch
+    if args.neg is not None:
+        w["K"] = args.neg
+    if args.dim:
+        w["d"] = args.dim
+    return w
+
+
+def build_model(w, E, R, rank, dev):
+    from KGE import optimizers
+    from KGE.models.semantic_based.RESCAL import RESCAL
+    from KGE.models.translating_based.RotatE import RotatE
+    from KGE.models.translating_based.TransE import TransE
+    from KGE.models.translating_based.TransR import TransR
+    from KGE.ns_strategy import UniformStrategy
+    d, K = w["d"], w["K"]
+    ns = UniformStrategy(np.arange(E), seed=12345 + rank)   # range(E): no device pool
+    kw = dict(loss_fn=w["loss"], ns_strategy=ns)
+    if w["model"] == "TransE":
+        m = TransE({"embedding_size": d}, K, w["side"], score_fn=w["score"], constraint=w["constraint"], **kw)
+    elif w["model"] == "RotatE":
+        m = RotatE({"embedding_size": d}, K, w["side"], score_fn=w["score"], **kw)
+    elif w["model"] == "RESCAL":
+        m = RESCAL({"embedding_size": d}, K, w["side"], constraint=w["constraint"], **kw)
+    else:
+        m = TransR({"ent_embedding_size": d, "rel_embedding_size": d}, K, w["side"], score_fn=w["score"],
+                   constraint=w["constraint"], **kw)
+    m.metadata = {"ind2ent": range(E), "ind2rel": range(R)}
+    m._model_weights_initial = None
+    if E > 10_000_000:
+        # the reference initialiser, drawn on the device (a host draw of 40 GB would dominate)
+        g = torch.Generator(device=dev).manual_seed(12345)
+        lim = 6.0 / np.sqrt(d)
+        m.model_weights = {"ent_emb": (torch.rand((E, d), generator=g, device=dev) * 2 - 1).mul_(lim),
+                           "rel_emb": (torch.rand((R, d), generator=g, device=dev) * 2 - 1).mul_(lim)}
+    else:
+        m._init_embeddings(seed=12345)          # identical init on every rank
+        m._to_device()
+    return m, optimizers.SGD(learning_rate=0.01)
+
+
+# ---------------------------------------------------------------- accounting
+def transe_bytes(B, K, d, E):
     """1 read + 1 write of every touched row occurrence."""
     step = 4 * d * (6 * B + 2 * B * K) + 12 * B
     score = 4 * d * (3 * B + B * K) + 12 * B          # KS: positive rows + one sampled row per negative
@@ -65,44 +150,91 @@ def algorithmic_bytes(B, K, d, E):
     return step, score, update, constrain
 
 
+def accounting(w, B, K, d, E, R, batch):
+    """Algorithmic work per step / per dominant-kernel launch."""
+    m = w["model"]
+    if m == "TransE":
+        step, score, upd, con = transe_bytes(B, K, d, E)
+        fused = w["constraint"]
+        return {"bound": "hbm", "step": step, "kernels": {"score_kernel": score,
+                                                           "update_kernel": upd + (con if fused else 0)}}
+    if m == "RotatE":
+        # entity rows 2d floats (8d bytes), relation rows d phases (4d bytes)
+        read = B * (2 * 8 * d + 4 * d) + B * K * 8 * d + 12 * B
+        return {"bound": "hbm", "step": 2 * read - 12 * B, "kernels": {"score_kernel": read,
+                                                                        "update_kernel": read - 12 * B}}
+    if m == "RESCAL":
+        ur = int(torch.unique(batch[:, 1]).numel())
+        sparse = 2 * (4 * d * (2 * B + B * K) + 4 * d * d * ur)
+        dense = 2 * 4 * (E * d + R * d * d)
+        return {"bound": "hbm", "step": sparse + dense, "distinct_relations": ur,
+                "kernels": {"score_kernel": 4 * d * (3 * B + B * K) + 12 * B}}
+    # TransR: three products per positive: P = X M (K+2 rows), S M^T (2K+4
+    # slice rows: every slice's ||M g||^2 is a clip_by_norm term), X^T S' (K+2)
+    flops = 2.0 * d * d * (4 * K + 8) * B
+    return {"bound": "mfma", "step_flops": flops, "kernels": {"transr_kernel": flops},
+            "survey_flops": 6.0 * d * d * (K + 2) * B}
+
+
+# ---------------------------------------------------------------- CPU baseline
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(triples, E, R, B, K, d, budget_s):
     """Time the CPU restatement (oracle, fp32 torch autograd on the host) on a
-    bounded sample: whole C2 steps until ~budget_s seconds of CPU work."""
+    bounded sample: whole C2 steps until ~budget_s seconds of CPU work, with
+    every core, then a shorter single-thread sample."""
     from oracle import kge_oracle as orc
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
     threads = min(threads, os.cpu_count() or threads)
-    torch.set_num_threads(threads)
     rng = np.random.default_rng(0)
-    W = {"ent_emb": rng.uniform(-6 / np.sqrt(d), 6 / np.sqrt(d), (E, d)).astype(np.float32),
-         "rel_emb": rng.uniform(-6 / np.sqrt(d), 6 / np.sqrt(d), (R, d)).astype(np.float32)}
-    n, t_total = 0, 0.0
-    while t_total < budget_s:
-        pos = triples[rng.integers(0, len(triples), B)]
-        neg = orc.uniform_negatives(pos, K, "h+t", E, seed=12345, plane=2 * n)
-        t0 = time.perf_counter()
-        out = orc.train_step("TransE", W, pos, neg, score=("lp", 2.0), loss=("sans", 3.0, 1.0), lr=0.01,
-                             constraint=True, dtype=torch.float32)
-        t_total += time.perf_counter() - t0
-        W = {k: v.astype(np.float32) for k, v in out["weights"].items()}
-        n += 1
-        if n >= 1 and t_total > budget_s:
-            break
-    return {"value": n * B / t_total, "unit": "positive-triples/s", "cores": threads, "kind": "port",
+
+    def run(nthreads, budget):
+        torch.set_num_threads(nthreads)
+        W = {"ent_emb": rng.uniform(-6 / np.sqrt(d), 6 / np.sqrt(d), (E, d)).astype(np.float32),
+             "rel_emb": rng.uniform(-6 / np.sqrt(d), 6 / np.sqrt(d), (R, d)).astype(np.float32)}
+        n, t_total = 0, 0.0
+        while t_total < budget:
+            pos = triples[rng.integers(0, len(triples), B)]
+            neg = orc.uniform_negatives(pos, K, "h+t", E, seed=12345, plane=2 * n)
+            t0 = time.perf_counter()
+            out = orc.train_step("TransE", W, pos, neg, score=("lp", 2.0), loss=("sans", 3.0, 1.0), lr=0.01,
+                                 constraint=True, dtype=torch.float32)
+            t_total += time.perf_counter() - t0
+            W = {k: v.astype(np.float32) for k, v in out["weights"].items()}
+            n += 1
+        return n, t_total
+
+    n, t = run(threads, budget_s)
+    n1, t1 = run(1, max(budget_s / 3, 3.0))
+    torch.set_num_threads(threads)
+    return {"value": n * B / t, "unit": "positive-triples/s", "cores": threads, "kind": "port",
+            "single_thread_value": n1 * B / t1, "cpu_model": cpu_model(), "nproc": os.cpu_count(),
             "sample": "%d whole C2 steps (B=%d, K=%d, d=%d, FB15k-237) of the fp32 torch-CPU restatement "
-                      "(oracle/kge_oracle.py), %.1f s" % (n, B, K, d, t_total)}
+                      "(oracle/kge_oracle.py) on %d threads, %.1f s; single thread: %d steps, %.1f s"
+                      % (n, B, K, d, threads, t, n1, t1)}
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the score kernel from the committed rocprofv3
+def pmc_traffic(workload):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
     --pmc summary (tools/pmc_traffic.py), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    name = "pmc_traffic.json" if workload == "c2" else "pmc_traffic_%s.json" % workload
     try:
-        with open(path) as f:
+        with open(os.path.join(ROOT, "profiles", name)) as f:
             return json.load(f)
     except (OSError, ValueError):
         return None
 
 
+# ---------------------------------------------------------------- main
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -115,21 +247,16 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from KGE import _hip, engine, loss, optimizers, score
-    from KGE.models.translating_based.TransE import TransE
-    from KGE.ns_strategy import UniformStrategy
+    from KGE import _hip, engine
     _hip.load()   # the shipped gfx950 library; raises if missing
 
+    w = spec(args.workload, args)
     triples, E, R = load_graph()
-    B, K, d = args.batch, args.neg, args.dim
-    model = TransE({"embedding_size": d}, K, "h+t", score_fn=score.LpDistance(p=2),
-                   loss_fn=loss.SelfAdversarialNegativeSamplingLoss(margin=3, temperature=1),
-                   ns_strategy=UniformStrategy(np.arange(E), seed=12345 + rank), constraint=True)
-    model.metadata = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
-    model._model_weights_initial = None
-    model._init_embeddings(seed=12345)          # identical init on every rank
-    model._to_device()
-    opt = optimizers.SGD(learning_rate=0.01)
+    synthetic = "E" in w
+    if synthetic:
+        E = w["E"]
+    B, K, d = w["B"], w["K"], w["d"]
+    model, opt = build_model(w, E, R, rank, dev)
     if world > 1:
         from KGE.sharded import ShardedStep
         step = ShardedStep(model)
@@ -138,9 +265,15 @@ def main():
 
     # batches resident in HBM before timing: a shuffled stream per rank
     nb = args.warmup + args.steps
-    g = torch.Generator().manual_seed(1000 + rank)
-    idx = torch.cat([torch.randperm(len(triples), generator=g) for _ in range((nb * B) // len(triples) + 1)])
-    batches = torch.from_numpy(triples)[idx[:nb * B]].reshape(nb, B, 3).to(dev)
+    if synthetic:
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        batches = torch.stack([torch.randint(0, E, (nb, B), generator=g, device=dev),
+                               torch.randint(0, R, (nb, B), generator=g, device=dev),
+                               torch.randint(0, E, (nb, B), generator=g, device=dev)], -1)
+    else:
+        g = torch.Generator().manual_seed(1000 + rank)
+        idx = torch.cat([torch.randperm(len(triples), generator=g) for _ in range((nb * B) // len(triples) + 1)])
+        batches = torch.from_numpy(triples)[idx[:nb * B]].reshape(nb, B, 3).to(dev)
 
     for s in range(args.warmup):
         step(batches[s], True, opt)
@@ -161,10 +294,10 @@ def main():
     step.check_status()
     ms = (t1 - t0) * 1e3 / args.steps
 
-    # per-kernel breakdown for the roofline: a second pass over the same
-    # batches with HIP events recorded on the step's own stream between the
-    # kernels [before K0, before KS, before KU, after KU]; the events cost a
-    # few us per step, so this pass never feeds `value`
+    # per-kernel breakdown: a second pass over the same batches with HIP events
+    # recorded on the step's own stream [before K0, before KS, after KS, after
+    # the update kernels]; the events cost a few us per step, so this pass
+    # never feeds `value`
     n_prof = min(args.steps, 100)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(n_prof)]
     for row in evs:
@@ -179,12 +312,6 @@ def main():
     k0 = float(np.mean([r[0].elapsed_time(r[1]) for r in evs]))
     ks = float(np.mean([r[1].elapsed_time(r[2]) for r in evs]))
     ku = float(np.mean([r[2].elapsed_time(r[3]) for r in evs]))
-    # single-GPU SGD + constraint: the renormalisation is fused into KS / KU
-    # (no K0 launch; its event pair brackets nothing) and KU also reads and
-    # writes every entity row
-    fused = world == 1
-    if fused:
-        k0 = 0.0
     if world > 1:
         t = torch.tensor([ms], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -193,36 +320,52 @@ def main():
         torch.distributed.destroy_process_group()
         return
 
-    step_b, score_b, upd_b, con_b = algorithmic_bytes(B, K, d, E)
-    kern = {"constrain_rows_kernel": {"ms": k0, "alg_bytes": con_b},
-            "score_kernel": {"ms": ks, "alg_bytes": score_b},
-            "update_kernel": {"ms": ku, "alg_bytes": upd_b + (con_b if fused else 0)}}
-    if fused:
-        del kern["constrain_rows_kernel"]
-    for v in kern.values():
-        v["GBps"] = v["alg_bytes"] / (v["ms"] * 1e-3) / 1e9
-    dom = max(kern, key=lambda k: kern[k]["ms"])
-    pmc = pmc_traffic()
-    traffic = None
-    if pmc and dom in pmc.get("kernels", {}):
-        traffic = pmc["kernels"][dom].get("hbm_bytes_per_launch")
-    roof = {"bound": "hbm", "kernel": dom, "achieved": round(kern[dom]["GBps"], 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(kern[dom]["GBps"] / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "step": {"alg_bytes": step_b, "kernel_ms": round(k0 + ks + ku, 5),
-                     "achieved": round(step_b / ((k0 + ks + ku) * 1e-3) / 1e9, 1),
-                     "frac": round(step_b / ((k0 + ks + ku) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-            "kernels": {k: {"ms": round(v["ms"], 5), "GBps": round(v["GBps"], 1)} for k, v in kern.items()}}
+    acc = accounting(w, B, K, d, E, R, batches[args.warmup])
+    names = list(acc["kernels"])
+    # event groups: KS group = the score pass (+ context / rank passes);
+    # KU group = update + apply passes
+    group_ms = {names[0]: ks}
+    if len(names) > 1:
+        group_ms[names[1]] = ku
+    if acc["bound"] == "hbm":
+        kern = {k: {"ms": round(group_ms[k], 5), "GBps": round(acc["kernels"][k] / (group_ms[k] * 1e-3) / 1e9, 1)}
+                for k in group_ms}
+        dom = names[0]
+        ach = acc["kernels"][dom] / (group_ms[dom] * 1e-3) / 1e9
+        pmc = pmc_traffic(args.workload)
+        traffic = None
+        if pmc and dom in pmc.get("kernels", {}):
+            traffic = pmc["kernels"][dom].get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "step": {"alg_bytes": acc["step"], "ms_per_step": round(ms, 5),
+                         "achieved": round(acc["step"] / (ms * 1e-3) / 1e9, 1),
+                         "frac": round(acc["step"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                "kernels": kern}
+        if "distinct_relations" in acc:
+            roof["distinct_relations"] = acc["distinct_relations"]
+    else:
+        dom = names[0]
+        tf = acc["kernels"][dom] / (ks * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": F32_MFMA_PEAK_TF,
+                "unit": "TFLOP/s", "frac": round(tf / F32_MFMA_PEAK_TF, 4), "traffic": None,
+                "flops_per_launch": acc["kernels"][dom], "survey_flops_per_step": acc["survey_flops"],
+                "step": {"ms_per_step": round(ms, 5), "achieved": round(acc["step_flops"] / (ms * 1e-3) / 1e12, 2)},
+                "kernels": {dom: {"ms": round(ks, 5)}, "update+apply": {"ms": round(ku, 5)},
+                            "constraint": {"ms": round(k0, 5)}}}
     cpu = None
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and args.workload == "c2" and not args.no_cpu_baseline:
         cpu = cpu_baseline(triples, E, R, B, K, d, args.cpu_seconds)
     value = world * B / (ms * 1e-3)
     out = {
-        "metric": "positive-triples/sec (batch x neg scored) at d=200, FB15k-237",
+        "metric": "positive-triples/sec (batch x neg scored) at d=%d, %s" % (d, "FB15k-237" if not synthetic else
+                                                                              "synthetic %d entities" % E),
         "value": round(value, 1), "unit": "positive-triples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "FB15k-237 train_indexed ids (real graph); random-init weights",
-        "config": {"workload": "C2: TransE d=%d, batch=%d, %d negs h+t, SANS(3,1), LpDistance(2), uniform, "
-                               "constraint, SGD" % (d, B, K), "global_batch": world * B,
+        "vs_baseline": None, "dtype": "f32",
+        "data": ("synthetic uniform ids over %d entities / %d relations; random-init weights" % (E, R)) if synthetic
+        else "FB15k-237 train_indexed ids (real graph); random-init weights",
+        "config": {"workload": w["desc"] % dict(B=B, K=K, d=d, E=E), "global_batch": world * B,
                    "negatives": K, "dim": d, "parallelism": "dp%d" % world,
                    "scored_triples_per_s": round(value * (1 + K), 1)},
         "roofline": roof, "cpu_baseline": cpu,
