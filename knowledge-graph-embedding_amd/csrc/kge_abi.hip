@@ -48,7 +48,7 @@ struct Plan {
   // dense-gradient / relation-matrix models (RESCAL)
   uint64_t o_upart, o_sorted, o_srel, o_gproj, o_rpart, o_regpart, o_gent, o_grel;
   uint64_t o_gneg, o_dm;   // TransR
-  uint64_t o_touched;
+  uint64_t o_touched, o_relseg;
   bool rescal, transr;
 };
 
@@ -301,6 +301,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
       P.o_grel = take((uint64_t)R * relc * 4);
     }
   }
+  if (rescal || transr) P.o_relseg = take((uint64_t)R * 2 * 4);
   if (transr) {
     P.o_sorted = take((uint64_t)B * 4);
     P.o_srel = take((uint64_t)B * 4);
@@ -432,6 +433,8 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     RA.B = A.B;
     RA.sorted = (int32_t*)(ws + P.o_sorted);
     RA.srel = (int32_t*)(ws + P.o_srel);
+    RA.rel_beg = (int32_t*)(ws + P.o_relseg);
+    RA.rel_cnt = RA.rel_beg + A.rel.rows;
     RA.status = A.status;
     TA.proj = TabView{d->rel_aux.data, d->rel_aux.ld, (int32_t)(d->dim * d->dim_rel), d->rel_aux.rows};
     TA.d = d->dim;
@@ -439,7 +442,8 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     TA.clip = d->constraint != 0;
     TA.dmpart = (float*)(ws + P.o_dm);
     TA.sorted = RA.sorted;
-    TA.srel = RA.srel;
+    TA.rel_beg = RA.rel_beg;
+    TA.rel_cnt = RA.rel_cnt;
     TA.gproj_out = d->optimizer == KGE_OPT_GRAD ? d->grad_out[2] : nullptr;
   }
   if (P.rescal) {
@@ -455,6 +459,8 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     RA.d = d->dim;
     RA.sorted = (int32_t*)(ws + P.o_sorted);
     RA.srel = (int32_t*)(ws + P.o_srel);
+    RA.rel_beg = (int32_t*)(ws + P.o_relseg);
+    RA.rel_cnt = RA.rel_beg + A.rel.rows;
     RA.snap = A.snap;
     RA.gpos = A.gpos;
     RA.gcols = A.gcols;

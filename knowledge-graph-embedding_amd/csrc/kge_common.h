@@ -318,7 +318,6 @@ __device__ __forceinline__ void store_row_half(const float (&h)[(VEC / 2 > 0 ? V
 // Phase profiling (profiling builds only, -DKGE_PHASE_PROF): thread 0 of each
 // workgroup adds the wall-clock ticks of each phase to a device counter.
 #ifdef KGE_PHASE_PROF
-extern __device__ unsigned long long g_kge_prof[64];
 #define KGE_PROF_INIT() unsigned long long kge_prof_t_ = threadIdx.x == 0 ? wall_clock64() : 0ull
 #define KGE_PROF(k)                                                   \
   do {                                                                \

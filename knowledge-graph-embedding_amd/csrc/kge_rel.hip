@@ -22,6 +22,8 @@
 // C[(l >> 4) * 4 + reg][l & 15]. fp32 in, fp32 accumulate (a k-ordered fmaf
 // chain): the same arithmetic as the reference's fp32 matmul up to summation
 // order.
+#include <algorithm>
+
 #include "kge_step.h"
 
 namespace kge {
@@ -39,45 +41,62 @@ __device__ __forceinline__ int64_t pos_id(const RelArgs& P, int64_t i, int c) {
 }
 
 // ------------------------------------------------------------ KR rank
-// rank_i = #{j : r_j < r_i} + #{j < i : r_j == r_i}; sorted[rank_i] = i
+// Thread t plays positive i = t and relation r = t:
+//   rank_i = #{j : r_j < r_i} + #{j < i : r_j == r_i};  sorted[rank_i] = i
+//   rel_beg[r] = #{j : r_j < r}, rel_cnt[r] = #{j : r_j == r}
+// Relation ids are staged 256 at a time in LDS and read back as int4
+// broadcasts (every lane reads the same address).
 __global__ __launch_bounds__(256) void rel_rank_kernel(RelArgs P) {
-  __shared__ int32_t s_r[256];
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int32_t ri = i < P.B ? (int32_t)pos_id(P, i, 1) : -1;
-  int64_t lt = 0, eq = 0;
+  __shared__ __attribute__((aligned(16))) int32_t s_r[256];
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int32_t ri = t < P.B ? (int32_t)pos_id(P, t, 1) : -1;
+  const int32_t rr = (int32_t)t;
+  int32_t lt = 0, eq = 0, rlt = 0, rcnt = 0;
   for (int64_t j0 = 0; j0 < P.B; j0 += 256) {
     __syncthreads();
     const int64_t j = j0 + threadIdx.x;
-    s_r[threadIdx.x] = j < P.B ? (int32_t)pos_id(P, j, 1) : 0;
+    s_r[threadIdx.x] = j < P.B ? (int32_t)pos_id(P, j, 1) : 0x7fffffff;   // sentinel: never < or ==
     __syncthreads();
-    const int n = (int)min<int64_t>(256, P.B - j0);
-    for (int q = 0; q < n; ++q) {
-      const int32_t x = s_r[q];
-      lt += x < ri ? 1 : 0;
-      eq += (x == ri && j0 + q < i) ? 1 : 0;
+    const int64_t before = t - j0;   // entries q < before precede positive t
+#pragma unroll 4
+    for (int q = 0; q < 256; q += 4) {
+      const int4 x = *reinterpret_cast<const int4*>(s_r + q);
+      lt += (x.x < ri) + (x.y < ri) + (x.z < ri) + (x.w < ri);
+      eq += (x.x == ri && q < before) + (x.y == ri && q + 1 < before) + (x.z == ri && q + 2 < before) +
+            (x.w == ri && q + 3 < before);
+      rlt += (x.x < rr) + (x.y < rr) + (x.z < rr) + (x.w < rr);
+      rcnt += (x.x == rr) + (x.y == rr) + (x.z == rr) + (x.w == rr);
     }
   }
-  if (i < P.B) {
-    P.sorted[lt + eq] = (int32_t)i;
+  if (t < P.B) {
+    P.sorted[lt + eq] = (int32_t)t;
     P.srel[lt + eq] = ri;
+  }
+  if (t < P.rel.rows) {
+    P.rel_beg[t] = rlt;
+    P.rel_cnt[t] = rcnt;
   }
 }
 
 // ------------------------------------------------------------ KC / KP pair products
-// One workgroup per leading sorted position of a 16-positive tile of one
-// relation (other positions exit at once). X1, X2 = 16 staged input rows.
+// Workgroup (p, g): p = a leading sorted position of a 16-positive tile of
+// one relation (other positions exit at once), g = a group of 4 of the
+// tile's 2 x ceil(d/16) output column tiles (one per wave). X1, X2 = the 16
+// staged input rows; each wave holds its column tile's whole B operand in
+// registers (inner dimension <= 256) before its MFMA chain.
 //   MODE 0 (context): X1 = h rows, X2 = t rows; out0 = X1 R (u), out1 = X2 R^T (v)
 //   MODE 1 (post):    X1 = B rows, X2 = A rows; out0 = X1 R (g_t), out1 = X2 R^T (g_h)
 template <int MODE>
 __global__ __launch_bounds__(256) void rel_pair_kernel(RelArgs P) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int d = P.d, D4 = (d + 3) & ~3;
-  const int64_t p = blockIdx.x;
+  const int d = P.d, D4 = (d + 3) & ~3, nct = (d + 15) / 16;
+  const int njg = (2 * nct + 3) / 4;
+  const int64_t p = blockIdx.x / njg;
+  const int g = (int)(blockIdx.x % njg);
   const int64_t r = P.srel[p];
-  const int64_t g0 = rel_lower(P.srel, 0, p + 1, r);
+  const int64_t g0 = P.rel_beg[r];
   if ((p - g0) % 16 != 0) return;
-  const int64_t g1 = rel_lower(P.srel, p, P.B, r + 1);
-  const int n = (int)min<int64_t>(16, g1 - p);
+  const int n = (int)min<int64_t>(16, g0 + P.rel_cnt[r] - p);
   float* X1 = sm;
   float* X2 = sm + 16 * D4;
   __shared__ int64_t s_i[16];
@@ -92,42 +111,45 @@ __global__ __launch_bounds__(256) void rel_pair_kernel(RelArgs P) {
         x1 = P.ent.row(pos_id(P, i, 0))[k];
         x2 = P.ent.row(pos_id(P, i, 2))[k];
       } else {
-        const float* g = P.gpos + i * 3 * (int64_t)P.gcols;
-        x1 = g[2 * P.gcols + k];   // B_i
-        x2 = g[k];                 // A_i
+        const float* gr = P.gpos + i * 3 * (int64_t)P.gcols;
+        x1 = gr[2 * P.gcols + k];   // B_i
+        x2 = gr[k];                 // A_i
       }
     }
     X1[e] = x1;
     X2[e] = x2;
   }
-  __syncthreads();
-  const float* Rm = P.rel.row(r);
   const int lane = lane_id(), wv = wave_id();
-  const int nct = (d + 15) / 16;
-  const int ar = lane & 15, kq = lane >> 4;
-  for (int job = wv; job < 2 * nct; job += 4) {
-    const int prod = job & 1, jt = job >> 1;
-    const int col = jt * 16 + (lane & 15);
-    const float* X = prod ? X2 : X1;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < D4; k0 += 4) {
-      const int k = k0 + kq;
-      const float a = X[ar * D4 + k];
-      float b = 0.f;
-      if (k < d && col < d) b = prod == 0 ? Rm[(int64_t)k * d + col] : Rm[(int64_t)col * d + k];
-      acc = mfma16(a, b, acc);
-    }
-    if (col < d) {
+  const int job = g * 4 + wv;
+  const bool has_job = job < 2 * nct;
+  const int prod = job & 1, jt = job >> 1;
+  const int col = jt * 16 + (lane & 15), kq = lane >> 4;
+  const int nks = D4 / 4;
+  const float* Rm = P.rel.row(r);
+  float bf[64];   // d <= 256 (plan check)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int row = kq * 4 + g;
-        if (row >= n) continue;
-        const int64_t i = s_i[row];
-        float* out;
-        if (MODE == 0) out = P.snap + i * 2 * (int64_t)d + (prod ? d : 0);
-        else out = P.gproj + i * 2 * (int64_t)d + (prod ? 0 : d);
-        out[col] = acc[g];
-      }
+  for (int ks = 0; ks < 64; ++ks) {
+    const int k = ks * 4 + kq;
+    bf[ks] = (has_job && ks < nks && k < d && col < d)
+                 ? (prod == 0 ? Rm[(int64_t)k * d + col] : Rm[(int64_t)col * d + k]) : 0.f;
+  }
+  __syncthreads();
+  if (!has_job) return;
+  const float* xa = (prod ? X2 : X1) + (lane & 15) * D4 + kq;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 64; ++ks)
+    if (ks < nks) acc = mfma16(xa[ks * 4], bf[ks], acc);
+  if (col < d) {
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const int row = kq * 4 + gg;
+      if (row >= n) continue;
+      const int64_t i = s_i[row];
+      float* out;
+      if (MODE == 0) out = P.snap + i * 2 * (int64_t)d + (prod ? d : 0);
+      else out = P.gproj + i * 2 * (int64_t)d + (prod ? 0 : d);
+      out[col] = acc[gg];
     }
   }
 }
@@ -148,7 +170,7 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
   __shared__ int64_t s_i[16];
   __shared__ float s_n2[4];
   __shared__ int s_last;
-  const int64_t beg = rel_lower(P.srel, 0, P.B, r), end = rel_lower(P.srel, beg, P.B, r + 1);
+  const int64_t beg = P.rel_beg[r], end = beg + P.rel_cnt[r];
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -283,15 +305,20 @@ __global__ __launch_bounds__(256) void reg_loss_kernel(TabView ent, TabView rel,
 
 // ------------------------------------------------------------ launchers
 void launch_rel_rank(const RelArgs& P, hipStream_t st) {
-  hipLaunchKernelGGL(rel_rank_kernel, dim3((unsigned)((P.B + 255) / 256)), dim3(256), 0, st, P);
+  const int64_t n = std::max<int64_t>(P.B, P.rel.rows);
+  hipLaunchKernelGGL(rel_rank_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P);
+}
+static unsigned pair_grid(const RelArgs& P) {
+  const int nct = (P.d + 15) / 16;
+  return (unsigned)(P.B * ((2 * nct + 3) / 4));
 }
 void launch_rel_ctx(const RelArgs& P, hipStream_t st) {
   const size_t lds = 2 * 16 * (size_t)((P.d + 3) & ~3) * sizeof(float);
-  hipLaunchKernelGGL(rel_pair_kernel<0>, dim3((unsigned)P.B), dim3(256), lds, st, P);
+  hipLaunchKernelGGL(rel_pair_kernel<0>, dim3(pair_grid(P)), dim3(256), lds, st, P);
 }
 void launch_rel_post(const RelArgs& P, hipStream_t st) {
   const size_t lds = 2 * 16 * (size_t)((P.d + 3) & ~3) * sizeof(float);
-  hipLaunchKernelGGL(rel_pair_kernel<1>, dim3((unsigned)P.B), dim3(256), lds, st, P);
+  hipLaunchKernelGGL(rel_pair_kernel<1>, dim3(pair_grid(P)), dim3(256), lds, st, P);
   const int nct = (P.d + 15) / 16;
   const size_t lds2 = (32 * 16 + 32 * (size_t)nct * 16) * sizeof(float);
   hipLaunchKernelGGL(rel_dr_kernel, dim3((unsigned)(P.rel.rows * nct)), dim3(256), lds2, st, P);

@@ -123,6 +123,8 @@ struct RelArgs {
   int32_t d;
   int32_t* sorted;           // [B] positives in relation order (stable)
   int32_t* srel;             // [B] relation of sorted position p
+  int32_t* rel_beg;          // [R] first sorted position of relation r
+  int32_t* rel_cnt;          // [R] positives of relation r
   float* snap;               // [B, 2, d] u = R^T h, v = R t
   const float* gpos;         // [B, 3, gcols] A, b, B (score kernel)
   int32_t gcols;
@@ -158,7 +160,8 @@ struct TrArgs {
   bool clip;         // constraint: projected vectors clipped to norm <= 1 (TransR.py:187-189)
   float* dmpart;     // [B, d * k] per-positive dM partials (summed per relation by the apply pass)
   const int32_t* sorted;
-  const int32_t* srel;
+  const int32_t* rel_beg;
+  const int32_t* rel_cnt;
   float* gproj_out;  // KGE_OPT_GRAD: dense [R, d * k] rel_proj gradient (else null)
 };
 constexpr int kTrWaves = 8;
@@ -173,8 +176,8 @@ struct TrLds {
 };
 __host__ __device__ inline TrLds tr_lds(int d, int k, int K) {
   TrLds L;
-  L.LX = ((d + 3) & ~3) + 1;
-  L.LP = ((k + 3) & ~3) + 1;
+  L.LX = ((d + 15) & ~15) + 1;   // rows padded to whole 16-column MFMA chunks (zero), odd stride
+  L.LP = ((k + 15) & ~15) + 1;
   L.NR16 = (K + 2 + 15) & ~15;
   L.SR16 = (2 * K + 4 + 15) & ~15;
   int o = L.NR16 * (L.LX + L.LP);

@@ -30,10 +30,6 @@
 
 namespace kge {
 
-#ifdef KGE_PHASE_PROF
-__device__ unsigned long long g_kge_prof[64];
-#endif
-
 // ------------------------------------------------------------ K0 constrain
 // kind 0: normalized_embeddings(p=2) -> X / pow(sum X^2, 1/2) * value
 // kind 1: clip_constraint(p=2)       -> rows with norm >= value rescaled

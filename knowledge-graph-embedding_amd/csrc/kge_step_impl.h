@@ -43,7 +43,9 @@
 namespace kge {
 
 #ifdef KGE_PHASE_PROF
-extern __device__ unsigned long long g_kge_prof[64];
+// one counter array per translation unit (no relocatable device code): each
+// profiled TU exports its own reader (kge_prof_read, kge_trprof_read)
+static __device__ unsigned long long g_kge_prof[64];
 #endif
 
 // ------------------------------------------------------------ helpers

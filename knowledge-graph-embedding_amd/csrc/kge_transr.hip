@@ -40,7 +40,7 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 constexpr int kTrQ = (kTrMaxSlots + kTrWaves - 1) / kTrWaves;   // slots per wave
 constexpr int kTrKV = kTrMaxDim / KGE_WAVE;                     // projected-row floats per lane
 constexpr int kTrKS = kTrMaxDim / 4;                            // MFMA k-steps held in registers
-constexpr int kTrKS3 = (kTrMaxSlots + 1 + 3) / 4;               // GEMM3 k-steps (K + 2 slot rows)
+constexpr int kTrKS3 = ((kTrMaxSlots + 1 + 15) / 16) * 4;       // GEMM3 k-steps (K + 2 slot rows, 16-padded)
 
 // element gradient of the score wrt a = x - y (Lp kinds): score_grad's rule
 template <int SK>
@@ -49,6 +49,36 @@ __device__ __forceinline__ float lp_elem_grad(float a, float alpha, float M) {
   float s = a > 0.f ? alpha : (a < 0.f ? -alpha : 0.f);
   if (SK == SK_PINF && fabsf(a) != M) s = 0.f;
   return s;
+}
+
+// all-lane sum / max over the wave (permlane + DPP tree, kge_common.h)
+__device__ __forceinline__ float wsum(float x) { return lane_reduce<5, false>(x); }
+__device__ __forceinline__ float wmax(float x) { return lane_reduce<5, true>(x); }
+
+// Two 16x16 output tiles sharing one B column (bf, in registers): A rows from
+// LDS at p0 / p1 (lane-adjusted: row l & 15, k offset l >> 4), 16 columns
+// (4 k-steps) per chunk, the chunk's A values read before its MFMAs so one
+// LDS wait covers 8 MFMAs, and two independent accumulator chains. Pad
+// columns of A and padded k-steps of bf are zero.
+template <int KS>
+__device__ __forceinline__ void mfma_pair_lds_a(f32x4& a0, f32x4& a1, const float* p0, const float* p1,
+                                                const float (&bf)[KS], int nkc) {
+#pragma unroll
+  for (int c = 0; c < KS / 4; ++c) {
+    if (c < nkc) {
+      float x0[4], x1[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        x0[u] = p0[(c * 4 + u) * 4];
+        x1[u] = p1[(c * 4 + u) * 4];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a0 = mfma16(x0[u], bf[c * 4 + u], a0);
+        a1 = mfma16(x1[u], bf[c * 4 + u], a1);
+      }
+    }
+  }
 }
 
 template <int SK>
@@ -74,6 +104,7 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
   int32_t* ids = reinterpret_cast<int32_t*>(sm + L.ids);
   float* misc = sm + L.misc;
 
+  KGE_PROF_INIT();
   const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
   const int64_t i = blockIdx.x;
   int err = 0;
@@ -87,12 +118,33 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
   __syncthreads();
   auto row_id = [&](int q) -> int64_t { return q == 0 ? ph : q == 1 ? pt : (int64_t)ids[q - 2]; };
 
-  // ---- gather X (pad rows and columns zero)
-  for (int row = wv; row < L.NR16; row += kTrWaves) {
-    const float* src = row < NR ? A.ent.row(row_id(row)) : nullptr;
-    for (int c = lane; c < D4; c += KGE_WAVE) X[row * LX + c] = (src && c < d) ? src[c] : 0.f;
+  KGE_PROF(32);
+  // ---- gather X (pad rows and columns zero): 4 rows' loads in flight per wave
+  for (int row0 = wv; row0 < L.NR16; row0 += 4 * kTrWaves) {
+    float v[4][kTrKV];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = row0 + u * kTrWaves;
+      const float* src = row < NR ? A.ent.row(row_id(row)) : nullptr;
+#pragma unroll
+      for (int c4 = 0; c4 < kTrKV; ++c4) {
+        const int c = lane + KGE_WAVE * c4;
+        v[u][c4] = (src && c < d) ? src[c] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int row = row0 + u * kTrWaves;
+      if (row >= L.NR16) break;
+#pragma unroll
+      for (int c4 = 0; c4 < kTrKV; ++c4) {
+        const int c = lane + KGE_WAVE * c4;
+        if (c < D4) X[row * LX + c] = v[u][c4];
+      }
+    }
   }
   __syncthreads();
+  KGE_PROF(33);
   // row statistics for the rel_proj slice norms: ||x||^2, x.h, x.t
   for (int row = wv; row < NR; row += kTrWaves) {
     float a = 0.f, b = 0.f, c2 = 0.f;
@@ -102,44 +154,48 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
       b += X[c] * x;
       c2 += X[LX + c] * x;
     }
-    a = wave_sum(a);
-    b = wave_sum(b);
-    c2 = wave_sum(c2);
+    a = wsum(a);
+    b = wsum(b);
+    c2 = wsum(c2);
     if (lane == 0) { xx[row] = a; xh[row] = b; xt[row] = c2; }
   }
 
-  // ---- GEMM1: P = X M_r
+  // ---- GEMM1: P = X M_r  (wave = 16-column tile of P; row tiles in pairs)
   const float* Mr = T.proj.row(pr);
   {
-    const int nct = (k + 15) / 16, nks = D4 / 4;
+    const int nct = (k + 15) / 16, nkc = (LX - 1) / 16, nrt = L.NR16 / 16;
     for (int ct = wv; ct < nct; ct += kTrWaves) {
       const int col = ct * 16 + (lane & 15);
       float bf[kTrKS];
 #pragma unroll
       for (int ks = 0; ks < kTrKS; ++ks) {
         const int kk = ks * 4 + (lane >> 4);
-        bf[ks] = (ks < nks && kk < d && col < k) ? Mr[(int64_t)kk * k + col] : 0.f;
+        bf[ks] = (kk < d && col < k) ? Mr[(int64_t)kk * k + col] : 0.f;
       }
-      for (int rt = 0; rt < L.NR16 / 16; ++rt) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        const float* xa = X + (rt * 16 + (lane & 15)) * LX + (lane >> 4);
-#pragma unroll
-        for (int ks = 0; ks < kTrKS; ++ks)
-          if (ks < nks) acc = mfma16(xa[ks * 4], bf[ks], acc);
+      for (int rt = 0; rt < nrt; rt += 2) {
+        const int rt1 = rt + 1 < nrt ? rt + 1 : rt;   // odd count: the last tile twice (discarded)
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+        const float* x0 = X + (rt * 16 + (lane & 15)) * LX + (lane >> 4);
+        const float* x1 = X + (rt1 * 16 + (lane & 15)) * LX + (lane >> 4);
+        mfma_pair_lds_a(a0, a1, x0, x1, bf, nkc);
         if (col < K4) {
 #pragma unroll
-          for (int g = 0; g < 4; ++g) P[(rt * 16 + (lane >> 4) * 4 + g) * LP + col] = acc[g];
+          for (int g = 0; g < 4; ++g) {
+            P[(rt * 16 + (lane >> 4) * 4 + g) * LP + col] = a0[g];
+            if (rt1 != rt) P[(rt1 * 16 + (lane >> 4) * 4 + g) * LP + col] = a1[g];
+          }
         }
       }
     }
   }
   __syncthreads();
 
+  KGE_PROF(34);
   // ---- clip the projected rows (TransR.py:187-189, constraint.py:94-99)
   for (int row = wv; row < NR; row += kTrWaves) {
     float s2 = 0.f;
     for (int c = lane; c < k; c += KGE_WAVE) s2 += P[row * LP + c] * P[row * LP + c];
-    const float n = sqrtf(wave_sum(s2));
+    const float n = sqrtf(wsum(s2));
     if (lane == 0) pn[row] = n;
     if (T.clip && !(n < 1.f)) {
       const float dv = fmaxf(n, 1e-9f);
@@ -160,6 +216,7 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
   auto yrow_of = [&](int q, int kind) { return kind == KIND_TC ? 2 + q : 1; };
   auto kind_of = [&](int q) { return q == K ? KIND_POS : slot_kind(A.side_mode, q); };
 
+  KGE_PROF(35);
   // ---- scores: s(x, y), x = P[xrow] + r, y = P[yrow]
   for (int m = 0; m < kTrQ; ++m) {
     const int q = wv + kTrWaves * m;
@@ -184,14 +241,14 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
         }
       }
     }
-    const float R = SK == SK_PINF ? wave_max(part) : wave_sum(part);
+    const float R = SK == SK_PINF ? wmax(part) : wsum(part);
     float ties = 1.f;
     if (SK == SK_PINF) {
       float tq = 0.f;
 #pragma unroll
       for (int v = 0; v < kTrKV; ++v)
         if (lane + KGE_WAVE * v < k && fabsf(av[v]) == R) tq += 1.f;
-      ties = wave_sum(tq);
+      ties = wsum(tq);
     }
     float lp;
     const float s = score_value<SK>(R, A.pw, &lp);
@@ -199,6 +256,7 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
   }
   __syncthreads();
 
+  KGE_PROF(36);
   // ---- loss and dL/ds per triple (one wave, IEEE transcendentals; every
   // weight decided once -- the backward below reuses it)
   if (wv == 0) {
@@ -207,11 +265,11 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
     float Ms = -INFINITY;
     if (sans)
       for (int q = lane; q < K; q += KGE_WAVE) Ms = fmaxf(Ms, A.temperature * sS[q]);
-    Ms = wave_max(Ms);
+    Ms = wmax(Ms);
     float Z = 0.f;
     if (sans)
       for (int q = lane; q < K; q += KGE_WAVE) Z += expf(A.temperature * sS[q] - Ms);
-    Z = wave_sum(Z);
+    Z = wsum(Z);
     const float invZ = sans ? (Z > 0.f ? 1.f / Z : 0.f) : 1.f;
     float lneg = 0.f, csum = 0.f;
     for (int q = lane; q < K; q += KGE_WAVE) {
@@ -229,8 +287,8 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
         default: lneg += s * s; break;
       }
     }
-    lneg = wave_sum(lneg);
-    csum = wave_sum(csum);
+    lneg = wsum(lneg);
+    csum = wsum(csum);
     if (lane == 0) {
       float lossp, cp;
       switch (A.loss_kind) {
@@ -254,6 +312,7 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
     for (int q = tid; q < K; q += kTrThreads) A.neg_score_out[i * K + q] = sS[q];
   __syncthreads();
 
+  KGE_PROF(37);
   float n_ent = 0.f, n_rel = 0.f, n_proj = 0.f;
   if (A.train) {
     // ---- per-triple gradients wrt the projected rows, back through the clip;
@@ -293,8 +352,8 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
         }
       }
       n_rel += gxx;
-      dx = wave_sum(dx);
-      dy = wave_sum(dy);
+      dx = wsum(dx);
+      dy = wsum(dy);
       // through clip_constraint: rows with norm >= 1 were divided by it
       const float nx = pn[xr], ny = pn[yr];
       const bool cx = T.clip && !(nx < 1.f), cy = T.clip && !(ny < 1.f);
@@ -310,9 +369,9 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
         b2 += gy[v] * gy[v];
         ab += gx[v] * gy[v];
       }
-      a2 = wave_sum(a2);
-      b2 = wave_sum(b2);
-      ab = wave_sum(ab);
+      a2 = wsum(a2);
+      b2 = wsum(b2);
+      ab = wsum(ab);
       // rel_proj slice of this triple: x_h (x) g_h + x_t (x) g_t
       const float hx = xx[xr], tx = xx[yr];
       const float htx = kind == KIND_POS ? xh[1] : (kind == KIND_TC ? xh[2 + q] : xt[2 + q]);
@@ -325,6 +384,7 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
       }
     }
     __syncthreads();   // P is dead from here: S overwrites X and P
+    KGE_PROF(38);
     // S rows: [0] sum of h-slices, [1] sum of t-slices, [2 + q] negative q's
     // entity slice, [K + 2] / [K + 3] the positive's h / t slices, [K + 4 + q]
     // negative q's positive-side slice; rows to SR16 zero
@@ -367,42 +427,51 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
     }
     __syncthreads();
 
+    KGE_PROF(39);
     // ---- GEMM2: Y = S M_r^T -> entity-row gradients and slice norms
     {
-      const int nct = (d + 15) / 16, nks = K4 / 4, nrt = (NS + 15) / 16;
+      const int nct = (d + 15) / 16, nkc = (LP - 1) / 16, nrt = (NS + 15) / 16;
+      float* gp2 = gp;
       for (int ct = wv; ct < nct; ct += kTrWaves) {
         const int col = ct * 16 + (lane & 15);
         float bf[kTrKS];
 #pragma unroll
         for (int ks = 0; ks < kTrKS; ++ks) {
           const int kk = ks * 4 + (lane >> 4);
-          bf[ks] = (ks < nks && kk < k && col < d) ? Mr[(int64_t)col * k + kk] : 0.f;
+          bf[ks] = (kk < k && col < d) ? Mr[(int64_t)col * k + kk] : 0.f;
         }
-        for (int rt = 0; rt < nrt; ++rt) {
-          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-          const float* sa = S + (rt * 16 + (lane & 15)) * LP + (lane >> 4);
-#pragma unroll
-          for (int ks = 0; ks < kTrKS; ++ks)
-            if (ks < nks) acc = mfma16(sa[ks * 4], bf[ks], acc);
+        for (int rt = 0; rt < nrt; rt += 2) {
+          const int rt1 = rt + 1 < nrt ? rt + 1 : rt;
+          f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+          const float* s0 = S + (rt * 16 + (lane & 15)) * LP + (lane >> 4);
+          const float* s1 = S + (rt1 * 16 + (lane & 15)) * LP + (lane >> 4);
+          mfma_pair_lds_a(acc[0], acc[1], s0, s1, bf, nkc);
           if (col < d) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const int row = rt * 16 + (lane >> 4) * 4 + g;
-              const float v = acc[g];
-              if (row == 0) gp[col] = v;
-              else if (row == 1) gp[2 * A.gcols + col] = v;
-              else if (row < NS) {
-                n_ent += v * v;
-                if (row < NR) A.gneg[(int64_t)(((uint32_t)i << A.kshift) | (uint32_t)(row - 2)) * d + col] = v;
+            for (int h = 0; h < 2; ++h) {
+              if (h == 1 && rt1 == rt) break;
+              const int rtt = h ? rt1 : rt;
+#pragma unroll
+              for (int g = 0; g < 4; ++g) {
+                const int row = rtt * 16 + (lane >> 4) * 4 + g;
+                const float v = acc[h][g];
+                if (row == 0) gp2[col] = v;
+                else if (row == 1) gp2[2 * A.gcols + col] = v;
+                else if (row < NS) {
+                  n_ent += v * v;
+                  if (row < NR) A.gneg[(int64_t)(((uint32_t)i << A.kshift) | (uint32_t)(row - 2)) * d + col] = v;
+                }
               }
             }
           }
         }
       }
     }
-    // ---- GEMM3: dM_i = X^T S[0 .. K+2) (X re-read from the table: L2)
+    KGE_PROF(40);
+    // ---- GEMM3: dM_i = X^T S[0 .. K+2) (X re-read from the table: L2); wave =
+    // 16-row tile of dM with its A column in registers, column tiles in pairs
     {
-      const int nrt = (d + 15) / 16, nct = (k + 15) / 16, nks = (NR + 3) / 4;
+      const int nrt = (d + 15) / 16, nct = (k + 15) / 16, nkc = (NR + 15) / 16;
       float* dm = T.dmpart + i * (int64_t)d * k;
       for (int rt = wv; rt < nrt; rt += kTrWaves) {
         const int ci = rt * 16 + (lane & 15);
@@ -410,25 +479,44 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
 #pragma unroll
         for (int ks = 0; ks < kTrKS3; ++ks) {
           const int kk = ks * 4 + (lane >> 4);
-          af[ks] = (ks < nks && kk < NR && ci < d) ? A.ent.row(row_id(kk))[ci] : 0.f;
+          af[ks] = (kk < NR && ci < d) ? A.ent.row(row_id(kk))[ci] : 0.f;
         }
-        for (int ct = 0; ct < nct; ++ct) {
-          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-          const float* sb = S + (lane >> 4) * LP + ct * 16 + (lane & 15);
+        for (int ct = 0; ct < nct; ct += 2) {
+          const int ct1 = ct + 1 < nct ? ct + 1 : ct;
+          f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+          const float* b0 = S + (lane >> 4) * LP + ct * 16 + (lane & 15);
+          const float* b1 = S + (lane >> 4) * LP + ct1 * 16 + (lane & 15);
 #pragma unroll
-          for (int ks = 0; ks < kTrKS3; ++ks)
-            if (ks < nks) acc = mfma16(af[ks], sb[ks * 4 * LP], acc);
-          const int col = ct * 16 + (lane & 15);
-          if (col < k) {
+          for (int c = 0; c < kTrKS3 / 4; ++c) {
+            if (c < nkc) {
+              float y0[4], y1[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                y0[u] = b0[(c * 4 + u) * 4 * LP];
+                y1[u] = b1[(c * 4 + u) * 4 * LP];
+              }
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                a0 = mfma16(af[c * 4 + u], y0[u], a0);
+                a1 = mfma16(af[c * 4 + u], y1[u], a1);
+              }
+            }
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            if (h == 1 && ct1 == ct) break;
+            const int col = (h ? ct1 : ct) * 16 + (lane & 15);
+            if (col >= k) continue;
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
               const int row = rt * 16 + (lane >> 4) * 4 + g;
-              if (row < d) dm[(int64_t)row * k + col] = acc[g];
+              if (row < d) dm[(int64_t)row * k + col] = (h ? a1 : a0)[g];
             }
           }
         }
       }
     }
+    KGE_PROF(41);
     // ---- destination keys for the update pass
     for (int q = tid; q < K; q += kTrThreads) bin_key(A, ids[q], ((uint32_t)i << A.kshift) | (uint32_t)q);
     if (tid < 3) {
@@ -437,11 +525,12 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
     }
   }
   if (err) set_status(A.status, err);
+  KGE_PROF(42);
 
   // ---- partials: loss, ||g||^2 per variable (0 ent, 1 rel_emb, 2 rel_proj);
   // the last workgroup reduces them in a fixed order
-  n_ent = wave_sum(n_ent);
-  n_rel = wave_sum(n_rel);
+  n_ent = wsum(n_ent);
+  n_rel = wsum(n_rel);
   if (lane == 0) { s_w[wv][0] = n_ent; s_w[wv][1] = n_rel; s_w[wv][2] = n_proj; }
   __syncthreads();
   if (tid == 0) {
@@ -467,7 +556,7 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
         acc[c] += __hip_atomic_load(&A.part[(int64_t)w * 8 + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #pragma unroll
-    for (int c = 0; c < 5; ++c) acc[c] = wave_sum(acc[c]);
+    for (int c = 0; c < 5; ++c) acc[c] = wsum(acc[c]);
     if (lane == 0) {
       A.loss_out[0] = acc[0];
       if (A.loss_accum) A.loss_accum[0] += acc[0];
@@ -491,7 +580,7 @@ __global__ __launch_bounds__(256) void transr_proj_apply(StepArgs A, TrArgs T) {
   const int64_t dk = (int64_t)T.d * T.k;
   const int64_t chunks = (dk + 1023) / 1024;
   const int64_t r = blockIdx.x / chunks, ch = blockIdx.x % chunks;
-  const int64_t beg = rel_lower(T.srel, 0, A.B, r), end = rel_lower(T.srel, beg, A.B, r + 1);
+  const int64_t beg = T.rel_beg[r], end = beg + T.rel_cnt[r];
   if (beg == end) return;
   const float sc = A.ctl->scale[2];
   const int64_t e1 = min(dk, (ch + 1) * 1024);
@@ -543,3 +632,13 @@ kge_status launch_step_transr(const StepArgs& A, const StepGeom& G, const TrArgs
 }
 
 }  // namespace kge
+
+#ifdef KGE_PHASE_PROF
+// profiling builds (tools/transr_prof.py): read / reset this TU's phase counters
+extern "C" int kge_trprof_read(unsigned long long* out, int n) {
+  if (n > 64) n = 64;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(kge::g_kge_prof), n * sizeof(unsigned long long)) != hipSuccess) return 1;
+  unsigned long long z[64] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(kge::g_kge_prof), z, sizeof(z)) != hipSuccess;
+}
+#endif
