@@ -99,7 +99,8 @@ def _native_plan_error(model, optimizer):
     return cache[key]
 
 
-FUSED_MODELS = (_hip.MODEL_TRANSE, _hip.MODEL_DISTMULT, _hip.MODEL_ROTATE, _hip.MODEL_RESCAL, _hip.MODEL_TRANSR)
+FUSED_MODELS = (_hip.MODEL_TRANSE, _hip.MODEL_DISTMULT, _hip.MODEL_ROTATE, _hip.MODEL_RESCAL, _hip.MODEL_TRANSR,
+                _hip.MODEL_TRANSH, _hip.MODEL_TRANSD)
 
 
 def fused_names(model):

@@ -52,6 +52,12 @@ class TransD(TranslatingModel):
         assert list(model_weights["ent_proj"].shape) == [E, ke], "shape of 'ent_proj' should be (len(metadata['ind2ent']), embedding_params['ent_embedding_size'])"
         assert list(model_weights["rel_proj"].shape) == [R, kr], "shape of 'rel_proj' should be (len(metadata['ind2rel']), embedding_params['rel_embedding_size'])"
 
+    def _fused_tables(self):
+        return {"ent": self.model_weights["ent_emb"], "rel": self.model_weights["rel_emb"],
+                "ent_aux": self.model_weights["ent_proj"], "rel_aux": self.model_weights["rel_proj"],
+                "dim": self.embedding_params["ent_embedding_size"],
+                "dim_rel": self.embedding_params["rel_embedding_size"]}
+
     def score_hrt(self, h, r, t):
         """``TransD.py:170-222``."""
         h, r, t = super(TransD, self).score_hrt(h, r, t)

@@ -54,6 +54,10 @@ class TransH(TranslatingModel):
         assert list(model_weights["rel_emb"].shape) == [R, k], "shape of 'rel_emb' should be (len(metadata['ind2rel']), embedding_params['embedding_size'])"
         assert list(model_weights["rel_hyper"].shape) == [R, k], "shape of 'rel_hyper' should be (len(metadata['ind2rel']), embedding_params['embedding_size'])"
 
+    def _fused_tables(self):
+        return {"ent": self.model_weights["ent_emb"], "rel": self.model_weights["rel_emb"],
+                "rel_aux": self.model_weights["rel_hyper"], "dim": self.embedding_params["embedding_size"]}
+
     def score_hrt(self, h, r, t):
         """``TransH.py:149-185``."""
         h, r, t = super(TransH, self).score_hrt(h, r, t)

@@ -7,7 +7,7 @@
 #include <cstdio>
 #include <string>
 
-#include "kge_step.h"
+#include "kge_proj.h"
 
 using namespace kge;
 
@@ -49,7 +49,8 @@ struct Plan {
   uint64_t o_upart, o_sorted, o_srel, o_gproj, o_rpart, o_regpart, o_gent, o_grel;
   uint64_t o_gneg, o_dm;   // TransR
   uint64_t o_touched, o_relseg;
-  bool rescal, transr;
+  uint64_t o_gnegp, o_gpos2, o_gdense[3], o_dpart;   // TransH / TransD
+  bool rescal, transr, proj, td, pj_dense;
 };
 
 int score_sk(int kind, float p) {
@@ -72,15 +73,16 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   if (d->abi_version != KGE_ABI_VERSION)
     return fail(KGE_EINVAL, "abi_version %d != library %d", d->abi_version, KGE_ABI_VERSION);
   const int model = d->model;
-  if (model != KGE_MODEL_TRANSE && model != KGE_MODEL_DISTMULT && model != KGE_MODEL_ROTATE &&
-      model != KGE_MODEL_RESCAL && model != KGE_MODEL_TRANSR)
+  if (model < KGE_MODEL_TRANSE || model > KGE_MODEL_RESCAL)
     return fail(KGE_EUNSUPPORTED, "model %d has no fused kernel in this build", model);
   if (d->dim <= 0) return fail(KGE_EINVAL, "dim must be > 0");
   const bool rescal = model == KGE_MODEL_RESCAL, transr = model == KGE_MODEL_TRANSR;
+  const bool td = model == KGE_MODEL_TRANSD, proj = td || model == KGE_MODEL_TRANSH;
   const int64_t entc = model == KGE_MODEL_ROTATE ? 2 * (int64_t)d->dim : d->dim;
-  // RESCAL: [R, d, d] matrices; TransR: rel_emb [R, k] (+ rel_proj [R, d, k] in rel_aux)
-  const int64_t relc = rescal ? (int64_t)d->dim * d->dim : transr ? d->dim_rel : d->dim;
-  if (transr && d->dim_rel <= 0) return fail(KGE_EINVAL, "dim_rel must be > 0");
+  // RESCAL: [R, d, d] matrices; TransR: rel_emb [R, k] (+ rel_proj [R, d, k] in rel_aux);
+  // TransD: rel_emb / rel_proj [R, k]
+  const int64_t relc = rescal ? (int64_t)d->dim * d->dim : (transr || td) ? d->dim_rel : d->dim;
+  if ((transr || td) && d->dim_rel <= 0) return fail(KGE_EINVAL, "dim_rel must be > 0");
   kge_status s;
   if ((s = check_table(d->ent, "ent_emb", entc))) return s;
   if ((s = check_table(d->rel, (model == KGE_MODEL_DISTMULT || rescal) ? "rel_inter" : "rel_emb", relc))) return s;
@@ -91,6 +93,15 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     if (!d->constraint)
       return fail(KGE_EUNSUPPORTED, "RESCAL with constraint=False (slice-norm clipping) has no fused kernel");
     if (d->dim > 256) return fail(KGE_EUNSUPPORTED, "RESCAL fused step supports d <= 256 (got %d)", d->dim);
+  }
+  if (proj) {
+    // TransH rel_hyper [R, d]; TransD rel_proj [R, k] + ent_proj [E, d]
+    if ((s = check_table(d->rel_aux, td ? "rel_proj" : "rel_hyper", relc))) return s;
+    if (d->rel_aux.rows != d->rel.rows) return fail(KGE_EINVAL, "rel_aux rows != rel_emb rows");
+    if (td) {
+      if ((s = check_table(d->ent_aux, "ent_proj", entc))) return s;
+      if (d->ent_aux.rows != d->ent.rows) return fail(KGE_EINVAL, "ent_proj rows != ent_emb rows");
+    }
   }
   if (transr) {
     if ((s = check_table(d->rel_aux, "rel_proj", (int64_t)d->dim * d->dim_rel))) return s;
@@ -121,8 +132,10 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   if (d->optimizer == KGE_OPT_SGD && !(d->clip_norm > 0.f)) return fail(KGE_EINVAL, "clip_norm must be > 0");
   if (d->optimizer == KGE_OPT_GRAD && (!d->grad_out[0] || !d->grad_out[1]))
     return fail(KGE_EINVAL, "KGE_OPT_GRAD needs grad_out[0] (ent) and grad_out[1] (rel)");
-  if (d->optimizer == KGE_OPT_GRAD && model == KGE_MODEL_TRANSR && !d->grad_out[2])
-    return fail(KGE_EINVAL, "KGE_OPT_GRAD needs grad_out[2] (rel_proj) for TransR");
+  if (d->optimizer == KGE_OPT_GRAD && (transr || proj) && !d->grad_out[2])
+    return fail(KGE_EINVAL, "KGE_OPT_GRAD needs grad_out[2] (rel_proj / rel_hyper)");
+  if (d->optimizer == KGE_OPT_GRAD && td && !d->grad_out[3])
+    return fail(KGE_EINVAL, "KGE_OPT_GRAD needs grad_out[3] (ent_proj) for TransD");
   if (d->optimizer == KGE_OPT_GRAD && !d->norm2_out) return fail(KGE_EINVAL, "KGE_OPT_GRAD needs norm2_out");
   if (!d->loss_out) return fail(KGE_EINVAL, "null loss_out");
   const kge_sampler_desc& sm = d->sampler;
@@ -154,6 +167,15 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     vec = (entc % 4 == 0 && d->ent.ld % 4 == 0 && relc % 2 == 0 && d->rel.ld % 2 == 0 && a16) ? 4 : 2;
     if (vec == 2 && !(d->ent.ld % 2 == 0 && aligned(d->ent.data, 8)))
       return fail(KGE_EINVAL, "RotatE ent_emb must be 8-byte aligned with even row stride");
+  } else if (proj) {
+    // every table of the projection family shares the fragment layout
+    const kge_table* tb[4] = {&d->ent, &d->rel, &d->rel_aux, &d->ent_aux};
+    auto all = [&](int m) {
+      for (int q = 0; q < (td ? 4 : 3); ++q)
+        if (tb[q]->cols % m != 0 || tb[q]->ld % m != 0 || !aligned(tb[q]->data, 4 * m)) return false;
+      return true;
+    };
+    vec = all(4) ? 4 : all(2) ? 2 : 1;
   } else {
     vec = (entc % 4 == 0 && relc % 4 == 0 && d->ent.ld % 4 == 0 && d->rel.ld % 4 == 0 && a16) ? 4 : 1;
   }
@@ -170,6 +192,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   if (nc > 4)
     return fail(KGE_EUNSUPPORTED, "row of %lld floats exceeds the fused kernel's %d", (long long)rowlen, 256 * vec);
   const int ncp = nc <= 1 ? 1 : nc <= 2 ? 2 : 4;
+  if (proj && ncp > 2)
+    return fail(KGE_EUNSUPPORTED, "row of %lld floats exceeds the projection kernel's %d", (long long)rowlen, 128 * vec);
 
   // score kernel: wpp waves per positive so that a wave streams <= 64 slots;
   // 8 / wpp positives per workgroup
@@ -217,7 +241,13 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.G.gridU = (int)ceil_div(nupd, kUpdWaves);
   P.rescal = rescal;
   P.transr = transr;
+  P.proj = proj;
+  P.td = td;
+  // TransH + constraint: the soft / orthogonality terms make every gradient dense
+  // (a validation step still adds their loss, BaseModel.py:319-323)
+  P.pj_dense = proj && !td && d->constraint;
   P.G.lds_score = (size_t)SL.total;
+  if (proj) P.G.lds_score = (size_t)pj_lds(Keff, FL, td).total * 4;
   if (P.G.lds_score > 160 * 1024)
     return fail(KGE_EUNSUPPORTED, "LDS budget exceeded (score kernel %zu bytes)", P.G.lds_score);
   P.sk = score_sk(d->score_kind, p);
@@ -235,6 +265,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.compact = compact;
   A.gent = d->grad_out[0];
   A.grel = d->grad_out[1];
+  A.grel_aux = d->grad_out[2];
+  A.gent_aux = d->grad_out[3];
   A.given = sm.kind == KGE_SAMPLER_GIVEN;
   A.pw = d->score_kind == KGE_SCORE_LP_POW;
   A.rel_half = model == KGE_MODEL_ROTATE;
@@ -277,14 +309,14 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
 
   uint64_t off = 0;
   auto take = [&](uint64_t bytes) { const uint64_t o = off; off += round_up((int64_t)bytes, 256); return o; };
-  const int nsnap = model == KGE_MODEL_ROTATE ? 3 : transr ? 0 : 2;
+  const int nsnap = model == KGE_MODEL_ROTATE ? 3 : (transr || proj) ? 0 : 2;
   // zero-state words first: control block, per-destination counters
   P.o_ctl = take(sizeof(StepCtl));
   P.o_cnt = take((uint64_t)ndest * 4);
   P.o_coef = take((uint64_t)(B << kshift) * 8);   // indexed by destination code
   P.o_snap = take((uint64_t)B * nsnap * entc * 4);
   P.o_gpos = take((uint64_t)B * 3 * rowlen * 4);
-  P.o_part = take((uint64_t)(transr ? std::max<int64_t>(nWG, B) : nWG) * 8 * 4);   // TransR: one partial per positive
+  P.o_part = take((uint64_t)((transr || proj) ? std::max<int64_t>(nWG, B) : nWG) * 8 * 4);   // one partial per positive
   P.o_list = take((uint64_t)ndest * cap * 4);
   P.o_ovf = take((uint64_t)T * 8);
   P.o_upart = take((uint64_t)P.G.gridU * 4);
@@ -307,6 +339,19 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     P.o_srel = take((uint64_t)B * 4);
     P.o_gneg = take((uint64_t)(B << kshift) * entc * 4);
     P.o_dm = take((uint64_t)B * d->dim * d->dim_rel * 4);
+  }
+  if (proj) {
+    P.o_gneg = take((uint64_t)(B << kshift) * entc * 4);
+    if (td) P.o_gnegp = take((uint64_t)(B << kshift) * entc * 4);
+    P.o_gpos2 = take((uint64_t)B * 3 * rowlen * 4);
+    if (P.pj_dense) {
+      if (d->optimizer == KGE_OPT_SGD) {   // KGE_OPT_GRAD: the caller's grad_out
+        P.o_gdense[0] = take((uint64_t)E * entc * 4);
+        P.o_gdense[1] = take((uint64_t)R * relc * 4);
+        P.o_gdense[2] = take((uint64_t)R * relc * 4);
+      }
+      P.o_dpart = take((uint64_t)kPjDenseWGs * 4 * 4);
+    }
   }
   P.ws_bytes = std::max<uint64_t>(off, 256);
   return KGE_OK;
@@ -473,12 +518,55 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     RA.status = A.status;
   }
 
+  PjPlan J{};
+  if (P.proj) {
+    A.gneg = (float*)(ws + P.o_gneg);
+    J.P.raux = TabView{d->rel_aux.data, d->rel_aux.ld, (int32_t)d->rel_aux.cols, d->rel_aux.rows};
+    J.raux_tab = J.P.raux;
+    if (P.td) {
+      J.P.eaux = TabView{d->ent_aux.data, d->ent_aux.ld, (int32_t)d->ent_aux.cols, d->ent_aux.rows};
+      J.eaux_tab = J.P.eaux;
+      J.P.gnegp = (float*)(ws + P.o_gnegp);
+    } else {
+      J.P.eaux = A.ent;   // never read
+    }
+    J.P.gpos2 = (float*)(ws + P.o_gpos2);
+    J.P.clip = P.td && d->constraint != 0;
+    J.P.kmin = std::min(d->dim, d->dim_rel > 0 ? d->dim_rel : d->dim);
+    J.td = P.td;
+    J.dense = P.pj_dense;
+    J.grads = P.pj_dense && d->optimizer != KGE_OPT_NONE;
+    J.lam = d->constraint_weight;
+    if (J.grads) {
+      for (int v = 0; v < 3; ++v)
+        J.gdense[v] = d->optimizer == KGE_OPT_GRAD ? d->grad_out[v] : (float*)(ws + P.o_gdense[v]);
+    }
+    if (P.pj_dense) J.dpart = (float*)(ws + P.o_dpart);
+  }
   hipEvent_t const* ev = (hipEvent_t const*)d->prof_events;
   if (ev) (void)hipEventRecord(ev[0], st);
   if (A.grad_mode && !P.rescal) {   // RESCAL's dense passes write every row
     (void)hipMemsetAsync(d->grad_out[0], 0, (size_t)A.ent.rows * A.ent.cols * sizeof(float), st);
     (void)hipMemsetAsync(d->grad_out[1], 0, (size_t)A.rel.rows * A.rel_gcols * sizeof(float), st);
     if (P.transr) (void)hipMemsetAsync(d->grad_out[2], 0, (size_t)TA.proj.rows * TA.proj.cols * sizeof(float), st);
+    if (P.proj) (void)hipMemsetAsync(d->grad_out[2], 0, (size_t)d->rel_aux.rows * d->rel_aux.cols * sizeof(float), st);
+    if (P.td) (void)hipMemsetAsync(d->grad_out[3], 0, (size_t)d->ent_aux.rows * d->ent_aux.cols * sizeof(float), st);
+  }
+  if (P.pj_dense && d->optimizer == KGE_OPT_SGD && d->batch > 0) {
+    // the update passes write only the touched rows of the dense gradients
+    (void)hipMemsetAsync(J.gdense[0], 0, (size_t)A.ent.rows * A.ent.cols * sizeof(float), st);
+    (void)hipMemsetAsync(J.gdense[1], 0, (size_t)A.rel.rows * A.rel.cols * sizeof(float), st);
+    (void)hipMemsetAsync(J.gdense[2], 0, (size_t)d->rel_aux.rows * d->rel_aux.cols * sizeof(float), st);
+  }
+  if (P.proj && d->constraint && !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT)) {
+    // _constraint_loss assigns: TransH normalises rel_hyper (TransH.py:202);
+    // TransD clips ent_emb and rel_emb (TransD.py:238-240)
+    const kge_table* tabs[2] = {P.td ? &d->ent : &d->rel_aux, &d->rel};
+    for (int v = 0; v < (P.td ? 2 : 1); ++v) {
+      const int64_t blocks = std::min<int64_t>(ceil_div(tabs[v]->rows, kWaves), 4096);
+      hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, tabs[v]->data,
+                         tabs[v]->rows, (int32_t)tabs[v]->cols, tabs[v]->ld, P.td ? 1 : 0, 1.0f);
+    }
   }
   if (P.transr && d->constraint && !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT)) {
     // _constraint_loss assigns (TransR.py:207-209): clip every entity and relation row to norm <= 1
@@ -503,7 +591,9 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     return hip_check("kge_step(empty batch)");
   }
   if (ev) (void)hipEventRecord(ev[1], st);
-  if (P.transr) {
+  if (P.proj) {
+    s = launch_step_proj(A, P.G, J, P.sk, st, ev);
+  } else if (P.transr) {
     s = launch_step_transr(A, P.G, TA, RA, P.sk, st, ev);
   } else if (P.rescal) {
     s = launch_step_rescal(A, P.G, RA, d->constraint ? d->constraint_weight : 0.f,

@@ -71,6 +71,12 @@ struct StepArgs {
   // kernel visits only those rows (untouched rows are not read or written)
   bool compact;
   uint32_t* touched;
+  // multi-table update passes (TransH / TransD): the aux-table pass runs
+  // first over the same destination lists and leaves the counters for the
+  // main pass; scale[] slots of the pass's entity / relation variable
+  bool keep_cnt = false;
+  bool rel_only = false;   // visit the relation destinations only (TransH rel_hyper pass)
+  int32_t sc_ent_idx = 0, sc_rel_idx = 1;
   // geometry
   int32_t wpp;      // waves per positive (1, 2, 4, 8)
   int32_t nP;       // positives per score workgroup = kStepWaves / wpp
@@ -92,6 +98,8 @@ struct StepArgs {
   // KGE_OPT_GRAD outputs: dense [E, ent.cols] / [R, rel_gcols]
   float* gent;
   float* grel;
+  float* gent_aux;  // TransD ent_proj (grad_out[3])
+  float* grel_aux;  // rel_hyper / rel_proj (grad_out[2])
   // outputs
   float* loss_out;
   float* loss_accum;

@@ -653,13 +653,13 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
     active = dd < (int64_t)A.ctl->touched_len;
     d = active ? (int64_t)A.touched[dd] : 0;
   } else {
-    active = dd < ndest;
+    active = dd < (A.rel_only ? R_ : ndest);
     d = dd < R_ ? E_ + dd : dd - R_;
   }
   const uint32_t nneg = A.nkeyneg;
   const uint32_t kmask = (1u << A.kshift) - 1u;
   const uint32_t snap_stride = (uint32_t)(M::NSNAP * A.snap_cols);   // B * stride < 2^32 (plan check)
-  const float sc_ent = A.ctl->scale[0], sc_rel = A.ctl->scale[1];   // issued up front
+  const float sc_ent = A.ctl->scale[A.sc_ent_idx], sc_rel = A.ctl->scale[A.sc_rel_idx];   // issued up front
 
   // one code -> its positive i and slot j (negative, c = -1) or row part c (0 h, 1 t, 2 r)
   auto decode = [&](uint32_t code, int64_t* i, int* j, int* c) {
@@ -760,7 +760,7 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
       }
     }
     if (n != 0u || (A.dense && is_ent)) {
-      if (lane == 0 && n != 0u) A.cnt[d] = 0u;   // ready for the next step
+      if (lane == 0 && n != 0u && !A.keep_cnt) A.cnt[d] = 0u;   // ready for the next step
       float racc[RV * NC];
 #pragma unroll
       for (int q = 0; q < RV * NC; ++q) racc[q] = 0.f;

@@ -29,10 +29,18 @@ def _make(model_name, d, K, side, score_fn, loss_fn, E, R, sampler, constraint=T
     from KGE.models.semantic_based.DistMult import DistMult
     from KGE.models.semantic_based.RESCAL import RESCAL
     from KGE.models.translating_based.RotatE import RotatE
+    from KGE.models.translating_based.TransD import TransD
     from KGE.models.translating_based.TransE import TransE
+    from KGE.models.translating_based.TransH import TransH
     from KGE.models.translating_based.TransR import TransR
     common = dict(loss_fn=loss_fn, ns_strategy=sampler)
-    if model_name == "TransE":
+    if model_name == "TransH":
+        m = TransH({"embedding_size": d}, K, side, score_fn=score_fn, constraint=constraint, constraint_weight=0.3,
+                   **common)
+    elif model_name == "TransD":
+        m = TransD({"ent_embedding_size": d, "rel_embedding_size": k or d}, K, side, score_fn=score_fn,
+                   constraint=constraint, **common)
+    elif model_name == "TransE":
         m = TransE({"embedding_size": d}, K, side, score_fn=score_fn, constraint=constraint, **common)
     elif model_name == "RotatE":
         m = RotatE({"embedding_size": d}, K, side, score_fn=score_fn, **common)
@@ -56,6 +64,16 @@ def _weights(model_name, E, R, d, rng, k=None):
         return {"ent_emb": rng.uniform(-0.5, 0.5, (E, d)).astype(np.float32),
                 "rel_emb": rng.uniform(-0.5, 0.5, (R, k)).astype(np.float32),
                 "rel_proj": (np.eye(d, k)[None] + rng.uniform(-0.2, 0.2, (R, d, k))).astype(np.float32)}
+    if model_name == "TransH":
+        return {"ent_emb": rng.uniform(-0.5, 0.5, (E, d)).astype(np.float32),
+                "rel_emb": rng.uniform(-0.5, 0.5, (R, d)).astype(np.float32),
+                "rel_hyper": rng.uniform(-0.5, 0.5, (R, d)).astype(np.float32)}
+    if model_name == "TransD":
+        k = k or d
+        return {"ent_emb": rng.uniform(-0.5, 0.5, (E, d)).astype(np.float32),
+                "rel_emb": rng.uniform(-0.5, 0.5, (R, k)).astype(np.float32),
+                "ent_proj": rng.uniform(-0.5, 0.5, (E, d)).astype(np.float32),
+                "rel_proj": rng.uniform(-0.5, 0.5, (R, k)).astype(np.float32)}
     if model_name == "RESCAL":
         return {"ent_emb": rng.uniform(-0.5, 0.5, (E, d)).astype(np.float32),
                 "rel_inter": rng.uniform(-0.2, 0.2, (R, d, d)).astype(np.float32)}
@@ -86,13 +104,15 @@ def _spec_loss(lf):
 
 
 def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, idx=torch.int64, train=True,
-             seed=11, constraint=True, typed=None, lr=0.05, opt="sgd", flags=0, k=None):
+             seed=11, constraint=True, typed=None, lr=0.05, opt="sgd", flags=0, k=None, pos=None):
     from KGE import engine, optimizers
     from KGE.ns_strategy import TypedStrategy, UniformStrategy
     dev = _dev()
     rng = np.random.default_rng(seed)
     W = _weights(model_name, E, R, d, rng, k)
-    pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+    if pos is None:
+        pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+    pos = np.asarray(pos, dtype=np.int64)
     if typed is None:
         sampler = UniformStrategy(np.arange(E), seed=seed)
     else:
@@ -242,7 +262,111 @@ def test_transr_validation_and_adam(hiplib):
     check(ref, got, l_, ps, ns)
 
 
-@pytest.mark.parametrize("model_name", ["TransE", "DistMult", "RotatE", "TransR"])
+@pytest.mark.parametrize("si", range(6))
+@pytest.mark.parametrize("li", range(5))
+def test_transh_matrix(hiplib, si, li):
+    """TransH (hyperplane projection, projection-family kernel) vs the oracle,
+    every score x loss; constraint on: rel_hyper renormalised, soft +
+    orthogonality terms make all three gradients dense."""
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransH", 24, 10, 6, "h+t", _scores()[si], _losses()[li])
+    check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("si", range(6))
+@pytest.mark.parametrize("li", range(5))
+def test_transd_matrix(hiplib, si, li):
+    """TransD (rank-1 r_p e_p^T + I projection, clipped) vs the oracle, every
+    score x loss, d != k (identity block of min(d, k))."""
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransD", 24, 10, 6, "h+t", _scores()[si], _losses()[li], k=20)
+    check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("model_name", ["TransH", "TransD"])
+@pytest.mark.parametrize("d,k,B,K,side,constraint", [(200, 200, 6, 64, "h+t", True), (32, 48, 17, 3, "t", True),
+                                                      (40, 16, 9, 5, "h", False), (17, 33, 5, 70, "h+t", True),
+                                                      (50, 50, 12, 1, "t", False), (200, 120, 3, 256, "h+t", False),
+                                                      (6, 6, 8, 9, "h+t", True)])
+def test_projection_shapes(hiplib, model_name, d, k, B, K, side, constraint):
+    """Row widths on every fragment layout (vec 4 / 2 / 1, one or two
+    chunks), K = 1 and K = 256, slots past a batch, constraint on / off."""
+    from KGE import loss, score
+    if model_name == "TransH":
+        k = None
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, model_name, d, B, K, side, score.LpDistancePow(2),
+                                          loss.SelfAdversarialNegativeSamplingLoss(2.0, 0.5), k=k,
+                                          constraint=constraint, E=90, R=4)
+    check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("model_name", ["TransH", "TransD"])
+@pytest.mark.parametrize("constraint", [True, False])
+def test_projection_validation_and_adam(hiplib, model_name, constraint):
+    from KGE import loss, score
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, model_name, 32, 12, 4, "h+t", score.LpDistancePow(2),
+                                          loss.PairwiseHingeLoss(1.0), train=False, constraint=constraint, k=24)
+    check(ref, got, l_, ps, ns)
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, model_name, 32, 12, 4, "h+t", score.LpDistance(2),
+                                          loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), opt="adam", lr=0.01,
+                                          constraint=constraint, k=24)
+    check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("model_name", ["TransH", "TransD"])
+def test_projection_consecutive_steps(hiplib, model_name):
+    """Three steps through one workspace (the aux pass keeps the lists for the
+    main pass, which then resets them) == three oracle steps."""
+    from KGE import engine, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    dev = _dev()
+    rng = np.random.default_rng(17)
+    E, R, d, B, K = 70, 5, 40, 13, 8
+    W = _weights(model_name, E, R, d, rng)
+    sampler = UniformStrategy(np.arange(E), seed=3)
+    m = _make(model_name, d, K, "h+t", score.LpDistance(1), loss.PairwiseHingeLoss(1.0), E, R, sampler)
+    m.model_weights = {k: torch.tensor(v, device=dev) for k, v in W.items()}
+    step = engine.FusedStep(m)
+    opt = optimizers.SGD(0.05)
+    ref_w = W
+    for it in range(3):
+        pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+        plane = sampler.offset
+        step(torch.tensor(pos, device=dev), True, opt)
+        torch.cuda.synchronize()
+        step.check_status()
+        neg = orc.negatives(pos, K, "h+t", E, seed=3, plane=plane)
+        ref = orc.train_step(model_name, ref_w, pos, neg, score=("lp", 1.0), loss=("hinge", 1.0), lr=0.05,
+                             constraint_weight=getattr(m, "constraint_weight", 1.0))
+        ref_w = ref["weights"]
+        assert abs(float(step.loss_out.item()) - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"])), it
+        for k, v in ref_w.items():
+            np.testing.assert_allclose(m.model_weights[k].cpu().numpy(), v, atol=TOL, err_msg="%s step %d" % (k, it))
+
+
+def test_c1_workload(hiplib):
+    """C1 exactly (BASELINE configs[0], example_fit_from_numpy.py pattern):
+    TransE d=50, B=128, K=1 corrupt_side='t', PairwiseHinge(1), LpDistance(2),
+    uniform, constraint, SGD -- on FB15k-237 ids from data/."""
+    import os
+    from KGE import loss, score
+    z = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data",
+                             "fb15k237_train.npz"))
+    X = z["triples"].astype(np.int64)
+    E, R = int(z["n_entities"]), int(z["n_relations"])
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransE", 50, 128, 1, "t", score.LpDistance(2),
+                                          loss.PairwiseHingeLoss(1.0), E=E, R=R, lr=0.01, pos=X[:128])
+    check(ref, got, l_, ps, ns)
+
+
+def test_rotate_k256_cross_wave_merge(hiplib):
+    """RotatE at C3's K = 256 (4 waves per positive: the cross-wave online
+    softmax merge of the complex accumulators) vs the oracle."""
+    from KGE import loss, score
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "RotatE", 64, 5, 256, "h+t", score.LpDistance(1),
+                                          loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E=400)
+    check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("model_name", ["TransE", "DistMult", "RotatE", "TransR", "TransH", "TransD"])
 def test_compact_update_large_table(hiplib, model_name):
     """E = 6000 rows vs 8 x (5 + 3) keys: the update kernel visits only the
     destinations the step touched (compact launch), untouched rows unchanged."""
