@@ -239,6 +239,58 @@ typedef struct kge_apply_desc {
   int64_t iteration;          /* ADAM step t >= 1 (optimizer.iterations + 1)   */
 } kge_apply_desc;
 
+/*
+ * Batched filtered ranking: KGEModel.evaluate / get_rank (BaseModel.py:578-654)
+ * for n evaluation triples at once. Query q ranks its true entity among all
+ * E candidates of the corrupted side:
+ *   rank[q] = 1 + #{ e : e not in filter(q), score(q, e) > score(q, true_q) }
+ * (strict >, the reference's tensor_scatter_nd_update(-inf) filter :650 and
+ * count :654; counted in int64 -- the reference's int16 overflows).
+ * The caller prepares each query's rows in the model's op order (KGE/engine.py
+ * rank_queries); the library scores the candidates:
+ *   KGE_RANK_TRANS  translating: P(e) = e (NONE), e - (w.e) w (HYPER, w = qw),
+ *                   clip(qw (e_p.e) + I e) (RANK1, e_p = cand_aux);
+ *                   't': s(q0, P(e)), 'h': s(P(e) + q0, q1)
+ *   KGE_RANK_ROT    RotatE complex rows: 't': s(q0, e), 'h': s(e o q0, q1)
+ *   KGE_RANK_MUL    DistMult: 't': sum(q0 * e), 'h': sum((e * q0) * q1)
+ *   KGE_RANK_DOT    sum(q0 * e) (RESCAL context rows)
+ * s = the score kind (score.py:49-89). filt_beg / filt_end index query q's
+ * filtered entities in filt_ent (ranges may be shared between queries; NULL =
+ * no filter). Stream-ordered; rank_out and pos_score_out are outputs.
+ */
+enum { KGE_RANK_TRANS = 0, KGE_RANK_ROT = 1, KGE_RANK_MUL = 2, KGE_RANK_DOT = 3 };
+enum { KGE_RPROJ_NONE = 0, KGE_RPROJ_HYPER = 1, KGE_RPROJ_RANK1 = 2 };
+
+typedef struct kge_rank_desc {
+  int32_t abi_version;        /* KGE_ABI_VERSION                                */
+  int32_t mode;               /* KGE_RANK_*                                     */
+  int32_t proj;               /* KGE_RPROJ_* (KGE_RANK_TRANS only)              */
+  int32_t corrupt_side;       /* KGE_SIDE_H or KGE_SIDE_T                       */
+  kge_table cand;             /* candidate rows [E, cols] (TransR: the group's projected table) */
+  kge_table cand_aux;         /* RANK1: ent_proj [E, cols]                      */
+  int32_t dim;                /* floats per query / projected row (RotatE: 2d)  */
+  int32_t clip;               /* RANK1: projected rows clipped to norm <= 1     */
+  const float* q0;            /* [n, ldq] query rows                            */
+  const float* q1;            /* [n, ldq] (h side / MUL; nullable otherwise)    */
+  const float* qw;            /* [n, ldq] HYPER w / RANK1 r_p (nullable)        */
+  int64_t ldq;
+  const void* true_ids;       /* [n] the true entity of each query (idx_dtype)  */
+  int32_t idx_dtype;          /* KGE_IDX_* of true_ids / filt_ent               */
+  int32_t score_kind;         /* KGE_SCORE_*                                    */
+  float score_p;              /* 1, 2 or +inf                                   */
+  int32_t _pad;
+  int64_t n;                  /* queries                                        */
+  const int64_t* filt_beg;    /* [n] (nullable: no filter)                      */
+  const int64_t* filt_end;    /* [n]                                            */
+  const void* filt_ent;       /* filtered entity ids (idx_dtype)                */
+  int64_t* rank_out;          /* [n]                                            */
+  float* pos_score_out;       /* [n] the true triples' scores                   */
+  int32_t* status;            /* device status word (nullable)                  */
+} kge_rank_desc;
+
+/* Batched filtered ranking (see kge_rank_desc). */
+kge_status kge_rank(const kge_rank_desc* d, void* stream);
+
 /* ABI version compiled into the library. */
 int32_t kge_abi_version(void);
 

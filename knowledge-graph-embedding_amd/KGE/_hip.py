@@ -21,6 +21,8 @@ IDX_I32, IDX_I64 = range(2)
 SAMPLER_UNIFORM, SAMPLER_TYPED, SAMPLER_GIVEN = range(3)
 OPT_NONE, OPT_SGD, OPT_GRAD, OPT_ADAM = range(4)
 FLAG_NO_TABLE_CONSTRAINT = 1
+RANK_TRANS, RANK_ROT, RANK_MUL, RANK_DOT = range(4)
+RPROJ_NONE, RPROJ_HYPER, RPROJ_RANK1 = range(3)
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libkge_hip.so")
 
@@ -76,8 +78,19 @@ class kge_apply_desc(ctypes.Structure):
                 ("_pad2", ctypes.c_int32), ("iteration", ctypes.c_int64)]
 
 
+class kge_rank_desc(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("mode", ctypes.c_int32), ("proj", ctypes.c_int32),
+                ("corrupt_side", ctypes.c_int32), ("cand", kge_table), ("cand_aux", kge_table),
+                ("dim", ctypes.c_int32), ("clip", ctypes.c_int32), ("q0", ctypes.c_void_p), ("q1", ctypes.c_void_p),
+                ("qw", ctypes.c_void_p), ("ldq", ctypes.c_int64), ("true_ids", ctypes.c_void_p),
+                ("idx_dtype", ctypes.c_int32), ("score_kind", ctypes.c_int32), ("score_p", ctypes.c_float),
+                ("_pad", ctypes.c_int32), ("n", ctypes.c_int64), ("filt_beg", ctypes.c_void_p),
+                ("filt_end", ctypes.c_void_p), ("filt_ent", ctypes.c_void_p), ("rank_out", ctypes.c_void_p),
+                ("pos_score_out", ctypes.c_void_p), ("status", ctypes.c_void_p)]
+
+
 EXPORTS = ("kge_abi_version", "kge_last_error", "kge_step_workspace_bytes", "kge_step", "kge_sample",
-           "kge_apply", "kge_constrain_rows")
+           "kge_apply", "kge_constrain_rows", "kge_rank")
 
 _lock = threading.Lock()
 _lib = None
@@ -104,6 +117,8 @@ def load(path=LIB_PATH):
         L.kge_sample.argtypes = [ctypes.POINTER(kge_sample_desc), ctypes.c_void_p]
         L.kge_apply.restype = ctypes.c_int
         L.kge_apply.argtypes = [ctypes.POINTER(kge_apply_desc), ctypes.c_void_p]
+        L.kge_rank.restype = ctypes.c_int
+        L.kge_rank.argtypes = [ctypes.POINTER(kge_rank_desc), ctypes.c_void_p]
         L.kge_constrain_rows.restype = ctypes.c_int
         L.kge_constrain_rows.argtypes = [kge_table, ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]
         if L.kge_abi_version() != ABI_VERSION:

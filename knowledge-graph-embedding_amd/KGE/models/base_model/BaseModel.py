@@ -349,7 +349,12 @@ class KGEModel:
     def evaluate(self, eval_X, corrupt_side, positive_X=None):
         """``BaseModel.py:578-618``."""
         X = np.asarray(eval_X) if not isinstance(eval_X, torch.Tensor) else eval_X.cpu().numpy()
-        ranks = [self.get_rank(X[k], positive_X, corrupt_side) for k in range(len(X))]
+        from ... import engine, ranking
+        if engine.backend() != "eager" and ranking.supported(self):
+            # the whole set in one pass on the device (kge_rank)
+            ranks = list(ranking.batched_ranks(self, X, corrupt_side, positive_X))
+        else:
+            ranks = [self.get_rank(X[k], positive_X, corrupt_side) for k in range(len(X))]
         return {
             "mean_rank": mean_rank(ranks),
             "mean_reciprocal_rank": mean_reciprocal_rank(ranks),

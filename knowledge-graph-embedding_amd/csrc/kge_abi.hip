@@ -641,6 +641,69 @@ kge_status kge_sample(const kge_sample_desc* d, void* stream) {
   return hip_check("kge_sample");
 }
 
+kge_status kge_rank(const kge_rank_desc* d, void* stream) {
+  if (!d) return fail(KGE_EINVAL, "null descriptor");
+  if (d->abi_version != KGE_ABI_VERSION)
+    return fail(KGE_EINVAL, "abi_version %d != library %d", d->abi_version, KGE_ABI_VERSION);
+  if (d->mode < KGE_RANK_TRANS || d->mode > KGE_RANK_DOT) return fail(KGE_EINVAL, "unknown rank mode %d", d->mode);
+  if (d->proj < KGE_RPROJ_NONE || d->proj > KGE_RPROJ_RANK1 || (d->proj != KGE_RPROJ_NONE && d->mode != KGE_RANK_TRANS))
+    return fail(KGE_EINVAL, "bad projection %d for rank mode %d", d->proj, d->mode);
+  if (d->corrupt_side != KGE_SIDE_H && d->corrupt_side != KGE_SIDE_T)
+    return fail(KGE_EINVAL, "corrupt_side must be 'h' or 't'");
+  if (d->n < 0) return fail(KGE_EINVAL, "n must be >= 0");
+  if (d->n == 0) return KGE_OK;
+  if (!d->cand.data || d->cand.rows <= 0 || d->cand.ld < d->cand.cols) return fail(KGE_EINVAL, "bad candidate table");
+  if (d->dim <= 0 || !d->q0 || d->ldq < d->dim || !d->true_ids || !d->rank_out || !d->pos_score_out)
+    return fail(KGE_EINVAL, "null query rows / ids / outputs");
+  const bool hside = d->corrupt_side == KGE_SIDE_H;
+  const bool rank1 = d->proj == KGE_RPROJ_RANK1, hyper = d->proj == KGE_RPROJ_HYPER;
+  if (hside && d->mode != KGE_RANK_DOT && !d->q1)
+    return fail(KGE_EINVAL, "q1 rows needed for corrupt_side 'h'");
+  if ((hyper || rank1) && !d->qw) return fail(KGE_EINVAL, "qw rows needed for the projection");
+  if (rank1 && (!d->cand_aux.data || d->cand_aux.rows != d->cand.rows || d->cand_aux.cols != d->cand.cols))
+    return fail(KGE_EINVAL, "RANK1 needs ent_proj rows shaped like the candidates");
+  if (d->mode == KGE_RANK_ROT && (d->dim % 2 || d->cand.cols != d->dim))
+    return fail(KGE_EINVAL, "RotatE rows are [d, 2] pairs");
+  if (!rank1 && d->cand.cols < d->dim) return fail(KGE_EINVAL, "candidate rows shorter than dim");
+  if ((d->filt_beg == nullptr) != (d->filt_end == nullptr) || (d->filt_beg && !d->filt_ent))
+    return fail(KGE_EINVAL, "filter needs filt_beg, filt_end and filt_ent");
+  const float p = d->score_p;
+  if (d->score_kind != KGE_SCORE_DOT && !(p == 1.f || p == 2.f || std::isinf(p)))
+    return fail(KGE_EUNSUPPORTED, "ranking Lp score supports p in {1, 2, inf} (got %g)", (double)p);
+  if (3 * kRankQ * ((d->dim + 3) & ~3) * 4 > 64 * 1024) return fail(KGE_EUNSUPPORTED, "query rows too wide");
+  RankArgs A{};
+  A.cand = d->cand.data;
+  A.cand_ld = d->cand.ld;
+  A.E = d->cand.rows;
+  A.caux = d->cand_aux.data;
+  A.caux_ld = d->cand_aux.ld;
+  A.dim = d->dim;
+  A.ecols = (int32_t)d->cand.cols;
+  A.kmin = (int32_t)std::min<int64_t>(d->dim, d->cand.cols);
+  A.clip = d->clip != 0;
+  A.hside = hside;
+  A.pw = d->score_kind == KGE_SCORE_LP_POW;
+  A.q0 = d->q0;
+  A.q1 = d->q1;
+  A.qw = d->qw;
+  A.ldq = d->ldq;
+  A.true_ids = d->true_ids;
+  A.i64 = d->idx_dtype == KGE_IDX_I64;
+  A.n = d->n;
+  A.fbeg = d->filt_beg;
+  A.fend = d->filt_end;
+  A.fent = d->filt_ent;
+  A.rank = (unsigned long long*)d->rank_out;
+  A.pos = d->pos_score_out;
+  A.status = d->status;
+  hipStream_t st = (hipStream_t)stream;
+  (void)hipMemsetAsync(d->rank_out, 0, (size_t)d->n * sizeof(int64_t), st);
+  const int sk = d->score_kind == KGE_SCORE_DOT ? SK_DOT : score_sk(d->score_kind, p);
+  if (launch_rank(A, d->mode, d->proj, sk, st) != KGE_OK)
+    return fail(KGE_EUNSUPPORTED, "no ranking instance for mode %d / score %d", d->mode, d->score_kind);
+  return hip_check("kge_rank");
+}
+
 kge_status kge_constrain_rows(kge_table t, int32_t kind, float value, void* stream) {
   if (!t.data || t.rows < 0 || t.cols <= 0 || t.ld < t.cols) return fail(KGE_EINVAL, "bad table");
   if (kind != 0 && kind != 1) return fail(KGE_EINVAL, "kind must be 0 (normalize) or 1 (clip)");

@@ -1,0 +1,262 @@
+// Batched filtered ranking for gfx950: KGEModel.evaluate / get_rank
+// (BaseModel.py:578-654) for a whole evaluation set in three launches.
+//
+// The reference ranks ONE triple per Python iteration (batch_size=1,
+// :598): it scores every entity on the corrupted side, overwrites the
+// filtered positives with -inf (:650) and counts scores strictly above the
+// true triple's (:654, int16). Here a query q is one evaluation triple; its
+// candidates are all E entities:
+//
+//   rank_pos_kernel     thread per query: the true entity's score through
+//                       the candidate scoring function (pos_score_out)
+//   rank_count_kernel   workgroup = 256 candidates (one per lane) x 8
+//                       queries; the queries' rows sit in LDS (broadcast
+//                       reads), each candidate row is loaded once per 8
+//                       queries and scored against all of them with no
+//                       cross-lane reduction (a lane owns its candidate's
+//                       whole sum); strict > pos per query -> ballot ->
+//                       popcount -> one int64 atomic per wave and query
+//   rank_filter_kernel  wave per query: rescores only its filtered entities
+//                       and subtracts those above the true score, + 1
+//
+// Every score is evaluated op by op (no contraction) in one fixed order, so
+// the true entity scored as a candidate equals its pos score bit for bit and
+// never counts itself, and the filter pass sees exactly the scores the count
+// pass compared. Counts are integer atomics (order-free, deterministic).
+//
+// Query rows are prepared by the host (KGE/engine.py rank_queries) with the
+// model's own op order: TransE t-side x = h + r; TransH x = P(h) + r with w_r;
+// TransD r_p; TransR the group's pre-projected candidate table; DistMult
+// h * r; RESCAL R^T h / R t; RotatE h o w / w, t.
+#include "kge_step.h"
+
+namespace kge {
+
+// Scores of candidate entity `e` against NQ queries whose rows sit at
+// q0 + j * qs, q1 + j * qs, w + j * qs (any address space). The candidate's
+// elements are loaded once and used by every query; each query's sum runs in
+// the same element order for any NQ, so NQ = 1 (pos / filter passes) and
+// NQ = 8 (count pass) give identical bits. MODE: KGE_RANK_*; PJ: KGE_RPROJ_*.
+template <int MODE, int PJ, int SK, int NQ>
+__device__ __forceinline__ void rank_scores(const RankArgs& A, int64_t e, const float* q0, const float* q1,
+                                            const float* w, int qs, float (&out)[NQ]) {
+#pragma clang fp contract(off)
+  const float* x = A.cand + e * A.cand_ld;
+  const int D = A.dim;
+  float acc[NQ];
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) acc[j] = 0.f;
+  auto lp = [&](float& ac, float a) {
+    const float m = fabsf(a);
+    if (SK == SK_P2) ac = ac + m * m;
+    else if (SK == SK_P1) ac = ac + m;
+    else ac = fmaxf(ac, m);
+  };
+  if (MODE == KGE_RANK_ROT) {
+    // complex pairs; t-side a = q0 - e, h-side a = e o q0 - q1
+    for (int c = 0; c < D; c += 2) {
+      const float er = x[c], ei = x[c + 1];
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const float* a0 = q0 + j * qs;
+        float ar, ai;
+        if (A.hside) {
+          const float* a1 = q1 + j * qs;
+          const float xr = er * a0[c] - ei * a0[c + 1];
+          const float xi = er * a0[c + 1] + ei * a0[c];
+          ar = xr - a1[c];
+          ai = xi - a1[c + 1];
+        } else {
+          ar = a0[c] - er;
+          ai = a0[c + 1] - ei;
+        }
+        if (SK == SK_P2) acc[j] = acc[j] + (ar * ar + ai * ai);
+        else {
+          const float m = sqrtf(ar * ar + ai * ai);
+          acc[j] = SK == SK_P1 ? acc[j] + m : fmaxf(acc[j], m);
+        }
+      }
+    }
+  } else if (MODE == KGE_RANK_MUL || MODE == KGE_RANK_DOT) {
+    // DistMult sum(h * r * t): t-side q0 = h * r, h-side (e * r) * t;
+    // RESCAL: q0 = R^T h (t-side) or R t (h-side)
+    for (int c = 0; c < D; ++c) {
+      const float xe = x[c];
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const float* a0 = q0 + j * qs;
+        acc[j] = acc[j] + ((MODE == KGE_RANK_MUL && A.hside) ? (xe * a0[c]) * q1[j * qs + c] : a0[c] * xe);
+      }
+    }
+  } else {
+    // translating: P(e) then t-side a = q0 - P(e), h-side a = (P(e) + q0) - q1
+    float dt[NQ], sc[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) { dt[j] = 0.f; sc[j] = 1.f; }
+    if (PJ == KGE_RPROJ_HYPER) {
+      for (int c = 0; c < D; ++c) {
+        const float xe = x[c];
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) dt[j] = dt[j] + w[j * qs + c] * xe;
+      }
+    } else if (PJ == KGE_RPROJ_RANK1) {
+      // e_p . e is the candidate's own; the clip norm depends on the query's r_p
+      const float* ep = A.caux + e * A.caux_ld;
+      float de = 0.f;
+      for (int c = 0; c < A.ecols; ++c) de = de + ep[c] * x[c];
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) dt[j] = de;
+      if (A.clip) {
+        float n2[NQ];
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) n2[j] = 0.f;
+        for (int c = 0; c < D; ++c) {
+          const float xe = c < A.kmin ? x[c] : 0.f;
+#pragma unroll
+          for (int j = 0; j < NQ; ++j) {
+            const float p = w[j * qs + c] * de + xe;
+            n2[j] = n2[j] + p * p;
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+          const float n = sqrtf(n2[j]);
+          if (!(n < 1.f)) sc[j] = fmaxf(n, 1e-9f);
+        }
+      }
+    }
+    for (int c = 0; c < D; ++c) {
+      const float xe = (PJ != KGE_RPROJ_RANK1 || c < A.kmin) ? x[c] : 0.f;
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) {
+        const float* a0 = q0 + j * qs;
+        float p;
+        if (PJ == KGE_RPROJ_HYPER) p = xe - dt[j] * w[j * qs + c];
+        else if (PJ == KGE_RPROJ_RANK1) p = (w[j * qs + c] * dt[j] + xe) / sc[j];
+        else p = xe;
+        if (SK == SK_DOT) acc[j] = acc[j] + (A.hside ? (p + a0[c]) * q1[j * qs + c] : a0[c] * p);
+        else lp(acc[j], A.hside ? (p + a0[c]) - q1[j * qs + c] : a0[c] - p);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) {
+    if (SK == SK_DOT || MODE == KGE_RANK_MUL || MODE == KGE_RANK_DOT) {
+      out[j] = acc[j];
+    } else {
+      float lpv;
+      out[j] = score_value<SK>(acc[j], A.pw, &lpv);
+    }
+  }
+}
+
+__device__ __forceinline__ const float* qrow(const float* base, const RankArgs& A, int64_t q) {
+  return base ? base + q * A.ldq : nullptr;
+}
+
+template <int MODE, int PJ, int SK>
+__global__ __launch_bounds__(256) void rank_pos_kernel(RankArgs A) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= A.n) return;
+  int64_t e = load_idx(A.true_ids, q, A.i64);
+  if (e < 0 || e >= A.E) { set_status(A.status, KGE_ERANGE); e = 0; }
+  float o[1];
+  rank_scores<MODE, PJ, SK, 1>(A, e, qrow(A.q0, A, q), qrow(A.q1, A, q), qrow(A.qw, A, q), 0, o);
+  A.pos[q] = o[0];
+}
+
+template <int MODE, int PJ, int SK>
+__global__ __launch_bounds__(kRankThreads) void rank_count_kernel(RankArgs A, int64_t nchunk) {
+  extern __shared__ __attribute__((aligned(16))) float qs[];
+  const int64_t g = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
+  const int64_t q0i = g * kRankQ;
+  const int nq = (int)min<int64_t>(kRankQ, A.n - q0i);
+  const int LQ = (A.dim + 3) & ~3;
+  float* s0 = qs;
+  float* s1 = qs + kRankQ * LQ;
+  float* sw = qs + 2 * kRankQ * LQ;
+  // the group's query rows (rows past the set: zeros, results discarded)
+  for (int t = threadIdx.x; t < kRankQ * A.dim; t += kRankThreads) {
+    const int q = t / A.dim, c = t % A.dim;
+    const bool v = q < nq;
+    s0[q * LQ + c] = v ? A.q0[(q0i + q) * A.ldq + c] : 0.f;
+    s1[q * LQ + c] = (v && A.q1) ? A.q1[(q0i + q) * A.ldq + c] : 0.f;
+    sw[q * LQ + c] = (v && A.qw) ? A.qw[(q0i + q) * A.ldq + c] : 0.f;
+  }
+  float pos[kRankQ];
+#pragma unroll
+  for (int q = 0; q < kRankQ; ++q) pos[q] = q < nq ? A.pos[q0i + q] : INFINITY;
+  __syncthreads();
+  const int64_t e = ch * kRankThreads + threadIdx.x;
+  const bool in = e < A.E;
+  const int64_t ee = in ? e : 0;
+  float s[kRankQ];
+  rank_scores<MODE, PJ, SK, kRankQ>(A, ee, s0, s1, sw, LQ, s);
+#pragma unroll
+  for (int q = 0; q < kRankQ; ++q) {
+    const unsigned long long m = __ballot(in && q < nq && s[q] > pos[q]);
+    if (lane_id() == 0 && m) atomicAdd(&A.rank[q0i + q], (unsigned long long)__popcll(m));
+  }
+}
+
+template <int MODE, int PJ, int SK>
+__global__ __launch_bounds__(256) void rank_filter_kernel(RankArgs A) {
+  const int64_t q = (int64_t)blockIdx.x * 4 + wave_id();
+  if (q >= A.n) return;
+  unsigned long long sub = 0;
+  if (A.fbeg) {
+    const float p = A.pos[q];
+    const float* r0 = qrow(A.q0, A, q);
+    const float* r1 = qrow(A.q1, A, q);
+    const float* rw = qrow(A.qw, A, q);
+    for (int64_t j = A.fbeg[q] + lane_id(); j < A.fend[q]; j += KGE_WAVE) {
+      const int64_t e = load_idx(A.fent, j, A.i64);
+      if (e < 0 || e >= A.E) { set_status(A.status, KGE_ERANGE); continue; }
+      float o[1];
+      rank_scores<MODE, PJ, SK, 1>(A, e, r0, r1, rw, 0, o);
+      sub += o[0] > p ? 1ull : 0ull;
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) sub += __shfl_xor(sub, o, KGE_WAVE);
+  if (lane_id() == 0) A.rank[q] = A.rank[q] - sub + 1ull;
+}
+
+template <int MODE, int PJ, int SK>
+static void rank_launch(const RankArgs& A, hipStream_t st) {
+  hipLaunchKernelGGL((rank_pos_kernel<MODE, PJ, SK>), dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, st, A);
+  const int64_t nchunk = (A.E + kRankThreads - 1) / kRankThreads;
+  const int64_t ng = (A.n + kRankQ - 1) / kRankQ;
+  const size_t lds = (size_t)3 * kRankQ * ((A.dim + 3) & ~3) * 4;
+  hipLaunchKernelGGL((rank_count_kernel<MODE, PJ, SK>), dim3((unsigned)(nchunk * ng)), dim3(kRankThreads), lds, st, A,
+                     nchunk);
+  hipLaunchKernelGGL((rank_filter_kernel<MODE, PJ, SK>), dim3((unsigned)((A.n + 3) / 4)), dim3(256), 0, st, A);
+}
+
+template <int MODE, int PJ>
+static void rank_by_sk(const RankArgs& A, int sk, hipStream_t st) {
+  switch (sk) {
+    case SK_P1: rank_launch<MODE, PJ, SK_P1>(A, st); break;
+    case SK_P2: rank_launch<MODE, PJ, SK_P2>(A, st); break;
+    case SK_PINF: rank_launch<MODE, PJ, SK_PINF>(A, st); break;
+    default: rank_launch<MODE, PJ, SK_DOT>(A, st); break;
+  }
+}
+
+kge_status launch_rank(const RankArgs& A, int mode, int proj, int sk, hipStream_t st) {
+  switch (mode) {
+    case KGE_RANK_TRANS:
+      if (proj == KGE_RPROJ_HYPER) rank_by_sk<KGE_RANK_TRANS, KGE_RPROJ_HYPER>(A, sk, st);
+      else if (proj == KGE_RPROJ_RANK1) rank_by_sk<KGE_RANK_TRANS, KGE_RPROJ_RANK1>(A, sk, st);
+      else rank_by_sk<KGE_RANK_TRANS, KGE_RPROJ_NONE>(A, sk, st);
+      return KGE_OK;
+    case KGE_RANK_ROT:
+      if (sk == SK_DOT) return KGE_EUNSUPPORTED;
+      rank_by_sk<KGE_RANK_ROT, KGE_RPROJ_NONE>(A, sk, st);
+      return KGE_OK;
+    case KGE_RANK_MUL: rank_launch<KGE_RANK_MUL, KGE_RPROJ_NONE, SK_DOT>(A, st); return KGE_OK;
+    case KGE_RANK_DOT: rank_launch<KGE_RANK_DOT, KGE_RPROJ_NONE, SK_DOT>(A, st); return KGE_OK;
+    default: return KGE_EUNSUPPORTED;
+  }
+}
+
+}  // namespace kge

@@ -209,6 +209,29 @@ kge_status launch_step_transr(const StepArgs& A, const StepGeom& G, const TrArgs
 kge_status launch_step_rescal(const StepArgs& A, const StepGeom& G, const RelArgs& P, float lam, float* regpart,
                               hipStream_t st, hipEvent_t const* ev);
 
+// ---- batched filtered ranking (kge_rank.hip): BaseModel.py:578-654
+constexpr int kRankQ = 8;          // queries per count workgroup
+constexpr int kRankThreads = 256;  // candidates per count workgroup
+
+struct RankArgs {
+  const float* cand; int64_t cand_ld; int64_t E;
+  const float* caux; int64_t caux_ld;    // TransD ent_proj
+  int32_t dim;                            // floats per query row / projected row
+  int32_t ecols;                          // floats per candidate row (RotatE 2d; TransD d)
+  int32_t kmin;                           // TransD identity block
+  bool clip;                              // TransD: projected rows clipped to norm <= 1
+  bool hside;                             // corrupt_side 'h'
+  bool pw;                                // LpDistancePow
+  const float* q0; const float* q1; const float* qw; int64_t ldq;
+  const void* true_ids; bool i64; int64_t n;
+  const int64_t* fbeg; const int64_t* fend; const void* fent;
+  unsigned long long* rank;
+  float* pos;
+  int32_t* status;
+};
+
+kge_status launch_rank(const RankArgs& A, int mode, int proj, int sk, hipStream_t st);
+
 __global__ void constrain_rows_kernel(float* t, int64_t rows, int32_t cols, int64_t ld, int kind,
                                       float value);
 

@@ -1,0 +1,120 @@
+"""GPU: batched filtered ranking (kge_rank, csrc/kge_rank.hip) vs the
+reference's per-triple get_rank (BaseModel.py:620-654) restated in torch on
+the same weights. Ranks are integers; they must be equal except where the
+per-triple path's own scores tie the true triple's within fp32 rounding
+(|s_e - s_true| <= 1e-5 max(1, |s_true|)), where a rank may move by at most
+the number of such near-ties."""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.test_plugin_surface import build, toy
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(autouse=True)
+def _fused(monkeypatch, hiplib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("KGE_BACKEND", "fused")
+
+
+def _per_triple(m, X, side, positive_X):
+    """Reference loop: ranks and the near-tie count of each query."""
+    ranks, ties = [], []
+    for x in X:
+        ranks.append(int(m.get_rank(x, positive_X, side)))
+        with torch.no_grad():
+            s = (m.score_hrt(h=None, r=x[1], t=x[2]) if side == "h" else m.score_hrt(h=x[0], r=x[1], t=None))
+            s = s.reshape(-1).double()
+            p = m.score_hrt(x[0:1], x[1:2], x[2:3]).reshape(()).double()
+        ties.append(int(torch.sum(torch.abs(s - p) <= 1e-5 * max(1.0, abs(float(p)))).item()))
+    return np.array(ranks), np.array(ties)
+
+
+def _check(got, ref, ties):
+    assert got.dtype == np.int64 and got.shape == ref.shape
+    assert (got >= 1).all()
+    bad = np.abs(got - ref) > ties
+    assert not bad.any(), (np.nonzero(bad)[0][:10], got[bad][:10], ref[bad][:10], ties[bad][:10])
+
+
+MODELS = ["TransE", "TransH", "TransR", "TransD", "RotatE", "DistMult", "RESCAL"]
+
+
+@pytest.mark.parametrize("name", MODELS)
+@pytest.mark.parametrize("side", ["h", "t"])
+def test_rank_toy_matches_get_rank(name, side, tmp_path):
+    from KGE import ranking, score
+    train, val, md = toy()
+    sc = None if name in ("DistMult", "RESCAL") else (score.LpDistance(1) if name == "RotatE" else score.LpDistance(2))
+    m = build(name, sc)
+    m.train(train_X=train, val_X=val, metadata=md, epochs=2, batch_size=4, optimizer="SGD", seed=7,
+            log_path=str(tmp_path))
+    assert ranking.supported(m)
+    X = np.concatenate([train, val])
+    for positive_X in (None, X):
+        got = ranking.batched_ranks(m, X, side, positive_X)
+        ref, ties = _per_triple(m, X, side, positive_X)
+        _check(got, ref, ties)
+
+
+@pytest.mark.parametrize("name,si", [("TransE", 1), ("TransE", 2), ("TransE", 3), ("TransH", 4), ("TransD", 5),
+                                     ("RotatE", 2), ("TransR", 3)])
+def test_rank_score_kinds(name, si, tmp_path):
+    """Every score kind the kernel instantiates (p = 1, 2, inf, Pow, Dot)."""
+    from KGE import ranking, score
+    train, val, md = toy()
+    s = [score.LpDistance(2), score.LpDistance(1), score.LpDistance(np.inf), score.LpDistancePow(2),
+         score.LpDistancePow(1), score.Dot()][si]
+    m = build(name, s)
+    m.train(train_X=train, val_X=val, metadata=md, epochs=1, batch_size=4, optimizer="SGD", seed=3,
+            log_path=str(tmp_path))
+    X = np.concatenate([train, val])
+    for side in ("h", "t"):
+        got = ranking.batched_ranks(m, X, side, X)
+        ref, ties = _per_triple(m, X, side, X)
+        _check(got, ref, ties)
+
+
+def test_evaluate_uses_kernel_and_metrics(tmp_path):
+    """evaluate() on the fused backend returns the reference's metric dict
+    computed from the kernel's ranks (same as the per-triple loop)."""
+    from KGE import ranking
+    train, val, md = toy()
+    m = build("TransE")
+    m.train(train_X=train, val_X=val, metadata=md, epochs=1, batch_size=4, optimizer="SGD", seed=1,
+            log_path=str(tmp_path))
+    r = m.evaluate(eval_X=val, corrupt_side="t", positive_X=np.concatenate([train, val]))
+    ranks = ranking.batched_ranks(m, val, "t", np.concatenate([train, val]))
+    assert r["mean_rank"] == pytest.approx(float(np.mean(ranks)))
+    assert r["hit@10"] == pytest.approx(float(np.mean(ranks <= 10)))
+
+
+def test_rank_fb15k237_slice_transe_d200():
+    """FB15k-237 graph (E = 14,541), TransE d = 200 with random weights: 300
+    triples ranked against all entities, filtered by the whole training set,
+    both sides, vs the per-triple path."""
+    from KGE import ranking, score
+    from KGE.models.translating_based.TransE import TransE
+    z = np.load(os.path.join(ROOT, "data", "fb15k237_train.npz"))
+    T = z["triples"].astype(np.int64)
+    E, R = int(z["n_entities"]), int(z["n_relations"])
+    m = TransE({"embedding_size": 200}, 1, "t", score_fn=score.LpDistance(2))
+    m.metadata = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
+    g = torch.Generator().manual_seed(0)
+    dev = torch.device("cuda", 0)
+    m.model_weights = {"ent_emb": ((torch.rand(E, 200, generator=g) - 0.5) * 0.2).to(dev),
+                       "rel_emb": ((torch.rand(R, 200, generator=g) - 0.5) * 0.2).to(dev)}
+    X = T[np.random.default_rng(1).choice(len(T), 300, replace=False)]
+    PX = torch.as_tensor(T, device=dev)
+    for side in ("h", "t"):
+        got = ranking.batched_ranks(m, X, side, PX)
+        ref, ties = _per_triple(m, X, side, T)
+        _check(got, ref, ties)
+        assert (got > 1).any()
