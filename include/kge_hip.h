@@ -291,6 +291,27 @@ typedef struct kge_rank_desc {
 /* Batched filtered ranking (see kge_rank_desc). */
 kge_status kge_rank(const kge_rank_desc* d, void* stream);
 
+/*
+ * Sparse SGD apply of one variable on listed rows (the owner-side update of
+ * the multi-GPU step, KGE/sharded.py): for i < n,
+ *   var[rows[i]] += -lr * clip_norm / max(sqrt(*norm2), clip_norm) * grad[i]
+ * (keras SGD ResourceScatterAdd after clip_by_norm, BaseModel.py:327-328).
+ * rows must be unique (the caller sums duplicates first); grad row stride
+ * grad_ld floats.
+ */
+typedef struct kge_apply_rows_desc {
+  kge_table var;              /* the owned rows (a shard)                       */
+  const int64_t* rows;        /* [n] local row indices, unique                  */
+  int64_t n;
+  const float* grad;          /* [n, grad_ld] summed gradient rows              */
+  int64_t grad_ld;
+  const float* norm2;         /* device [1]: global ||g slices||^2 of the variable */
+  float lr;
+  float clip_norm;
+} kge_apply_rows_desc;
+
+kge_status kge_apply_rows(const kge_apply_rows_desc* d, void* stream);
+
 /* ABI version compiled into the library. */
 int32_t kge_abi_version(void);
 

@@ -89,8 +89,14 @@ class kge_rank_desc(ctypes.Structure):
                 ("pos_score_out", ctypes.c_void_p), ("status", ctypes.c_void_p)]
 
 
+class kge_apply_rows_desc(ctypes.Structure):
+    _fields_ = [("var", kge_table), ("rows", ctypes.c_void_p), ("n", ctypes.c_int64), ("grad", ctypes.c_void_p),
+                ("grad_ld", ctypes.c_int64), ("norm2", ctypes.c_void_p), ("lr", ctypes.c_float),
+                ("clip_norm", ctypes.c_float)]
+
+
 EXPORTS = ("kge_abi_version", "kge_last_error", "kge_step_workspace_bytes", "kge_step", "kge_sample",
-           "kge_apply", "kge_constrain_rows", "kge_rank")
+           "kge_apply", "kge_constrain_rows", "kge_rank", "kge_apply_rows")
 
 _lock = threading.Lock()
 _lib = None
@@ -117,6 +123,8 @@ def load(path=LIB_PATH):
         L.kge_sample.argtypes = [ctypes.POINTER(kge_sample_desc), ctypes.c_void_p]
         L.kge_apply.restype = ctypes.c_int
         L.kge_apply.argtypes = [ctypes.POINTER(kge_apply_desc), ctypes.c_void_p]
+        L.kge_apply_rows.restype = ctypes.c_int
+        L.kge_apply_rows.argtypes = [ctypes.POINTER(kge_apply_rows_desc), ctypes.c_void_p]
         L.kge_rank.restype = ctypes.c_int
         L.kge_rank.argtypes = [ctypes.POINTER(kge_rank_desc), ctypes.c_void_p]
         L.kge_constrain_rows.restype = ctypes.c_int

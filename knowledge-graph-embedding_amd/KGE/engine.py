@@ -251,7 +251,10 @@ class FusedStep:
         t = self._tables()
         key = (int(batch.shape[0]), batch.dtype, bool(is_train), id(optimizer),
                getattr(optimizer, "learning_rate", None), neg_ids is not None,
-               pos_score is not None, neg_score is not None, t["ent"].data_ptr(), t["rel"].data_ptr(),
+               pos_score is not None, neg_score is not None,
+               tuple((t[r].data_ptr(), tuple(t[r].shape), t[r].stride(0)) if t.get(r) is not None else None
+                     for r in ("ent", "rel", "ent_aux", "rel_aux")),
+               tuple((g.data_ptr(), tuple(g.shape)) for g in self.grads) if self.grads is not None else None,
                id(m.ns_strategy), m.negative_ratio, m.corrupt_side, self.batch_scale, self.flags)
         cached = getattr(self, "_cache", None)
         if cached is not None and cached[0] == key:

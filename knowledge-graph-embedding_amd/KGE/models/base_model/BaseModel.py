@@ -295,6 +295,7 @@ class KGEModel:
         """``CheckpointManager(max_to_keep=1).save()`` (``BaseModel.py:248-253``)."""
         os.makedirs(self.log_path, exist_ok=True)
         path = os.path.join(self.log_path, "ckpt.pt")
+        self.sync_weights()   # multi-GPU: the shards are the authoritative entity rows
         torch.save({k: v.detach().cpu() for k, v in self.model_weights.items()}, path)
         return path
 
@@ -304,6 +305,8 @@ class KGEModel:
         with torch.no_grad():
             for k, v in saved.items():
                 self.model_weights[k].copy_(v.to(self.model_weights[k].device))
+        if self._fused is not None and hasattr(self._fused, "load"):
+            self._fused.load(saved)   # multi-GPU: into every rank's shard
 
     def _check_early_stopping(self, metric_history, magnitude, patience_now, patience_max, step,
                               restore_best_weight=True):

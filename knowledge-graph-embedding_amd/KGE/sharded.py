@@ -1,43 +1,45 @@
-"""Multi-GPU training step: data-parallel over triples, entity table row-sharded.
+"""Multi-GPU training step: data-parallel over triples, entity tables row-sharded.
 
 The reference is single-device (``BaseModel.py:19-21``); this is the build's
 one parallel strategy. One process per GPU,
 ``torch.distributed`` with the RCCL backend ("nccl" on ROCm) over xGMI.
 
-Layout in HBM, per rank g of G:
-  * ``shard``  [Es, cols]   rows [g*Es, (g+1)*Es) of ent_emb (block ownership,
-                            Es = ceil(E / G)); the authoritative copy.
-  * ``full``   [G*Es, cols] the gathered table the kernels read this step
-                            (``model_weights['ent_emb']`` views its first E rows).
-  * ``gfull``  [G*Es, cols] this rank's dense entity gradient; ``gshard`` its
-                            reduce-scattered owner slice.
-  * relation tables are replicated (<= 38 MB even for RESCAL / TransR);
-    their gradient travels in ``red`` with the per-variable slice norm^2 and
-    the loss, in ONE all-reduce.
+Ownership: entity row ``e`` lives on rank ``e mod G`` at local row ``e div G``
+(modulo keeps FB15k-237's degree load within 1.05x at G = 8; id blocks give
+2.24x because ``index_kg`` numbers entities in first-appearance order). The
+entity tables of a model (``ent_emb``, TransD's ``ent_proj``) share one
+``shard`` buffer, row = [ent | ent_aux]. Relation tables are replicated.
 
-One step (``ShardedStep.__call__``), every rank with its own positives:
-  1. ``_constraint_loss`` table assigns on the owned rows (TransE / DistMult
-     renormalisation, ``TransE.py:171-172``) -- before scoring, as
-     ``BaseModel.py:319`` orders it;
-  2. all-gather shards -> ``full``;
-  3. ``kge_step`` in ``KGE_OPT_GRAD`` mode on ``full`` (sampling with a
-     rank-disjoint counter plane, gather, score, loss normalised by the GLOBAL
-     batch via ``batch_scale = G``, gradients, slice norm^2);
-  4. all-reduce ``red`` = [rel grad | norm^2 x4 | loss];
-  5. reduce-scatter ``gfull`` -> ``gshard``;
-  6. ``kge_apply`` (clip_by_norm with the global norm, SGD / Adam) on the
-     shard and on the replicated relation table.
-G ranks x B positives therefore compute the step one device would compute
-on the concatenated G*B batch (up to float summation order).
-
-Whenever every row is touched each step (uniform negatives at FB15k-237
-scale touch all 14,505 rows), this dense exchange moves the same bytes as a
-de-duplicated all-to-all of requested rows, with fixed sizes and no host
-sync. The collectives go through ``Exchange``, which uses the tensor forms
-RCCL provides and, for the gloo CPU tests of this logic, list / all-reduce
-forms with the same results.
+One step (``ShardedStep.__call__``), every rank with its own B positives:
+  0. ``_constraint_loss`` assigns on the owned rows (TransE / DistMult
+     renormalise, TransR / TransD clip; ``BaseModel.py:319`` order) and on the
+     replicated relation tables;
+  1. negatives drawn with ``kge_sample`` from rank-disjoint counter planes;
+  2. exchange the rows the batch needs into a local row cache:
+     * ``sparse`` (default for tables > 1 GiB, C5): sort + unique of the
+       batch's ids, one ``all_to_all_single`` of per-owner counts, one of the
+       ids, the owners gather their rows, one ``all_to_all_single`` of the rows
+       back -- the cache holds exactly the unique rows, in request order;
+     * ``dense`` (small tables, FB15k-237 scale where every row is touched
+       anyway): ``all_gather_into_tensor`` of the shards -- fixed sizes, no
+       host sync;
+  3. ``kge_step`` in ``KGE_OPT_GRAD`` mode on the cache (ids remapped to cache
+     rows, negatives given): gather, score, loss normalised by the GLOBAL
+     batch (``batch_scale = G``), duplicate-summed gradient rows of the cache,
+     per-variable slice norm^2;
+  4. one ``all_reduce`` of [relation gradients | norm^2 x4 | loss];
+  5. the cache's gradient rows go back to their owners (``all_to_all_single``
+     with the request splits reversed / ``reduce_scatter_tensor``);
+  6. owners sum each row's contributions in source-rank order (unique indices
+     per source: deterministic) and apply clip_by_norm with the global norm
+     + SGD on the touched rows only (``kge_apply_rows``; Adam: dense keras
+     Adam over the shard, ``kge_apply``); the replicated relation tables get
+     the same ``kge_apply`` on every rank.
+G ranks x B positives compute the step one device computes on the
+concatenated G*B batch with the same negatives (up to float summation order).
 """
 
+import ctypes
 import math
 
 import torch
@@ -46,13 +48,16 @@ import torch.distributed as dist
 from . import _hip
 from . import engine
 from . import optimizers as _opt
-from .constraint import normalized_embeddings
+from .constraint import clip_constraint, normalized_embeddings
 
 _RENORM = (_hip.MODEL_TRANSE, _hip.MODEL_DISTMULT)
+_CLIP = (_hip.MODEL_TRANSR, _hip.MODEL_TRANSD)
+DENSE_TABLE_BYTES = 1 << 30   # "auto": all-gather below this entity-table size
 
 
 class Exchange:
-    """The step's collectives on one process group."""
+    """The step's collectives on one process group (tensor forms on RCCL; the
+    gloo CPU tests of this logic get list forms with the same results)."""
 
     def __init__(self, group=None):
         self.group = group
@@ -70,93 +75,231 @@ class Exchange:
         if self.tensor_forms:
             dist.reduce_scatter_tensor(shard, full, op=dist.ReduceOp.SUM, group=self.group)
         else:
-            dist.all_reduce(full, group=self.group)
-            shard.copy_(full.chunk(self.world)[self.rank])
+            t = full.clone()
+            dist.all_reduce(t, group=self.group)
+            shard.copy_(t.chunk(self.world)[self.rank])
 
     def all_reduce(self, t):
         dist.all_reduce(t, group=self.group)
+
+    def all_to_all(self, out, inp, out_splits=None, in_splits=None):
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
 
 class ShardedStep:
     """Drop-in for ``FusedStep`` across G ranks (see module docstring)."""
 
-    def __init__(self, model, exchange=None):
+    def __init__(self, model, exchange=None, mode="auto"):
         self.model = model
         self.ex = exchange or Exchange()
         G, g = self.ex.world, self.ex.rank
-        self.names = engine.fused_names(model) if hasattr(model, "_fused_tables") else \
-            {"ent": "ent_emb", "rel": _rel_name(model)}
-        ent = model.model_weights[self.names["ent"]]
-        rel = model.model_weights[self.names["rel"]]
-        self.ent_shape = tuple(ent.shape)
+        self.G, self.g = G, g
+        t = model._fused_tables()
+        self.tables = t
+        self.names = engine.fused_names(model)
+        ent = t["ent"]
         E = int(ent.shape[0])
-        cols = ent.numel() // E
-        Es = -(-E // G)
+        self.E = E
+        self.ent_shape = tuple(ent.shape)
+        self.ce = ent.numel() // E
+        self.aux_shape = tuple(t["ent_aux"].shape) if t.get("ent_aux") is not None else None
+        self.ca = t["ent_aux"].numel() // E if self.aux_shape else 0
+        C = self.ce + self.ca
+        self.C = C
+        self.Es = -(-E // G)
+        self.valid = len(range(g, E, G))
         dev = ent.device
-        self.E, self.Es, self.lo = E, Es, g * Es
-        self.valid = max(0, min(Es, E - self.lo))
-        self.full = torch.zeros(G * Es, cols, dtype=torch.float32, device=dev)
-        self.full[:E] = ent.reshape(E, cols)
-        self.shard = self.full[self.lo:self.lo + Es].clone()
-        self.gfull = torch.zeros(G * Es, cols, dtype=torch.float32, device=dev)
-        self.gshard = torch.zeros(Es, cols, dtype=torch.float32, device=dev)
-        model.model_weights[self.names["ent"]] = self.full[:E].view(self.ent_shape)
-        R = int(rel.shape[0])
-        self.rel_cols = rel.numel() // R
-        nrel = R * self.rel_cols
-        self.red = torch.zeros(nrel + 8, dtype=torch.float32, device=dev)
-        self.grel = self.red[:nrel].view(R, self.rel_cols)
-        self.norm2 = self.red[nrel:nrel + 4]
-        self.loss = self.red[nrel + 4:nrel + 5]
-        self.renorm = model._fused_model_id in _RENORM and bool(getattr(model, "constraint", False))
+        self.device = dev
+        self.mid = model._fused_model_id
+        if self.mid == _hip.MODEL_RESCAL or (self.mid == _hip.MODEL_TRANSH and getattr(model, "constraint", False)):
+            raise NotImplementedError("sharded step: full-table regulariser gradients (RESCAL, TransH with "
+                                      "constraint) are not sharded in this build")
+        if mode == "auto":
+            mode = "dense" if E * C * 4 <= DENSE_TABLE_BYTES else "sparse"
+        if mode not in ("dense", "sparse"):
+            raise ValueError("mode must be 'auto', 'dense' or 'sparse'")
+        self.mode = mode
+        # owned rows [ent | ent_aux], padded to Es rows
+        self.shard = torch.zeros(self.Es, C, dtype=torch.float32, device=dev)
+        self.shard[:self.valid, :self.ce] = ent.reshape(E, -1)[g::G]
+        if self.ca:
+            self.shard[:self.valid, self.ce:] = t["ent_aux"].reshape(E, -1)[g::G]
+        if mode == "dense":
+            self.full = torch.zeros(G * self.Es, C, dtype=torch.float32, device=dev)
+            self.gfull = [torch.zeros(G * self.Es, c, dtype=torch.float32, device=dev) for c in self._ecols()]
+            self.gshard = [torch.zeros(self.Es, c, dtype=torch.float32, device=dev) for c in self._ecols()]
+        # replicated relation tables and the all-reduce buffer
+        self.rel_roles = [r for r in ("rel", "rel_aux") if t.get(r) is not None]
+        sizes = [t[r].numel() for r in self.rel_roles]
+        self.red = torch.zeros(sum(sizes) + 8, dtype=torch.float32, device=dev)
+        self.grel, o = {}, 0
+        for r, n in zip(self.rel_roles, sizes):
+            self.grel[r] = self.red[o:o + n].view(t[r].shape[0], -1)
+            o += n
+        self.norm2 = self.red[o:o + 4]
+        self.loss = self.red[o + 4:o + 5]
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        c = getattr(model, "constraint", False)
+        self.renorm = self.mid in _RENORM and bool(c)
+        self.clip = self.mid in _CLIP and bool(c)
+        self.hyper = self.mid == _hip.MODEL_TRANSH and bool(c)
         self.fused = None
+        self._cap = 0
         if dev.type == "cuda":
-            f = engine.FusedStep(model, grad_mode=True)
-            f.grads = [self.gfull[:E], self.grel]
+            self.lib = _hip.lib()
+            f = engine.FusedStep(model, grad_mode=True, tables=dict(t))
             f.norm2 = self.norm2
             f.loss_out = self.loss
+            f.status = self.status
             f.batch_scale = float(G)
-            f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT if self.renorm else 0
-            f.plane_fn = lambda ns, n: ns.take_planes(n) * G + g * n
+            f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT
             self.fused = f
         elif engine.backend() != "eager":
             raise RuntimeError("ShardedStep needs GPUs (or KGE_BACKEND=eager for host-only tests)")
 
-    # ------------------------------------------------------------ phases
-    def _constrain_shard(self):
-        if not self.renorm or self.valid == 0:
-            return
-        rows = self.shard[:self.valid]
-        if self.fused is not None:
-            _hip.check(self.fused.lib.kge_constrain_rows(_hip.table(rows), 0, 1.0,
-                                                         _hip.stream_handle(rows.device)), "kge_constrain_rows")
-        else:
-            rows.copy_(normalized_embeddings(rows, p=2, value=1, axis=1))
+    def _ecols(self):
+        return [self.ce] + ([self.ca] if self.ca else [])
 
-    def _local_grads(self, batch, is_train, neg_ids, optimizer, prof_events=None):
+    # ------------------------------------------------------------ phases
+    def _constrain(self):
+        """_constraint_loss assigns (BaseModel.py:319): owned entity rows, and
+        the replicated relation tables identically on every rank."""
+        rows = self.shard[:self.valid, :self.ce]
+        rel = self.tables["rel"]
         if self.fused is not None:
-            self.fused(batch, is_train, optimizer if is_train else None, neg_ids=neg_ids, prof_events=prof_events)
+            st = _hip.stream_handle(self.device)
+            if self.renorm and self.valid:
+                _hip.check(self.lib.kge_constrain_rows(_hip.table(rows), 0, 1.0, st), "kge_constrain_rows")
+            if self.clip:
+                if self.valid:
+                    _hip.check(self.lib.kge_constrain_rows(_hip.table(rows), 1, 1.0, st), "kge_constrain_rows")
+                _hip.check(self.lib.kge_constrain_rows(_hip.table(rel), 1, 1.0, st), "kge_constrain_rows")
+            if self.hyper:
+                _hip.check(self.lib.kge_constrain_rows(_hip.table(self.tables["rel_aux"]), 0, 1.0, st),
+                           "kge_constrain_rows")
+            return
+        with torch.no_grad():
+            if self.renorm and self.valid:
+                rows.copy_(normalized_embeddings(rows, p=2, value=1, axis=1))
+            if self.clip:
+                rows.copy_(clip_constraint(rows, p=2, value=1, axis=-1))
+                rel.copy_(clip_constraint(rel, p=2, value=1, axis=-1))
+
+    def _draw(self, batch):
+        """Negatives in the step's slot layout (h+t: alternating h / t draws,
+        BaseModel.py:353-356) from rank-disjoint planes (kge_sample)."""
+        m = self.model
+        ns = m.ns_strategy
+        two = m.corrupt_side == "h+t"
+        p0 = ns.take_planes(2 if two else 1) * self.G + self.g * (2 if two else 1)
+        K = int(m.negative_ratio)
+        Ks = K // 2 if two else K
+        B = int(batch.shape[0])
+        i64 = batch.dtype == torch.int64
+        outs = []
+        for k, side in enumerate(("h", "t") if two else (m.corrupt_side,)):
+            out = torch.empty(B * Ks, dtype=batch.dtype, device=batch.device)
+            d = _hip.kge_sample_desc()
+            d.sampler = ns.sampler_desc(_hip.IDX_I64 if i64 else _hip.IDX_I32, batch.device, p0 + k)
+            d.X = batch.data_ptr()
+            d.n = B
+            d.side = _hip.SIDE_H if side == "h" else _hip.SIDE_T
+            d.negative_ratio = Ks
+            d.out = out.data_ptr()
+            d.status = self.status.data_ptr()
+            _hip.check(self.lib.kge_sample(d, _hip.stream_handle(batch.device)), "kge_sample")
+            outs.append(out)
+        if not two:
+            return outs[0]
+        return torch.stack([outs[0].view(B, Ks), outs[1].view(B, Ks)], dim=-1).reshape(-1)
+
+    def _fetch_sparse(self, ids):
+        """Unique ids -> row cache in request order + the remap of ``ids``."""
+        G, g, ex = self.G, self.g, self.ex
+        uniq = torch.unique(ids)
+        own = uniq % G
+        order = torch.argsort(own, stable=True)
+        req = uniq[order]
+        send = torch.bincount(own, minlength=G)
+        recv = torch.empty_like(send)
+        ex.all_to_all(recv, send)
+        sc, rc = send.tolist(), recv.tolist()       # the one host sync of the step
+        rids = torch.empty(sum(rc), dtype=req.dtype, device=req.device)
+        ex.all_to_all(rids, req, rc, sc)
+        rows = self.shard[torch.div(rids, G, rounding_mode="floor")]
+        U = int(req.shape[0])
+        cache = self._cache_buf(U)
+        ex.all_to_all(cache, rows, sc, rc)
+        inv = torch.empty_like(order)
+        inv[order] = torch.arange(U, device=order.device)
+        remap = inv[torch.searchsorted(uniq, ids)]
+        return cache, remap, (sc, rc, rids)
+
+    def _cache_buf(self, U):
+        if U > self._cap:
+            self._cap = max(U, int(self._cap * 1.25))
+            self._cache = torch.empty(self._cap, self.C, dtype=torch.float32, device=self.device)
+            self._gcache = [torch.empty(self._cap, c, dtype=torch.float32, device=self.device) for c in self._ecols()]
+        return self._cache[:U]
+
+    def _local_tables(self, cache):
+        """The model's tables with the entity tables replaced by cache views."""
+        t = dict(self.tables)
+        U = cache.shape[0]
+        ent = cache[:, :self.ce]
+        t["ent"] = ent if len(self.ent_shape) == 2 else ent.view((U,) + self.ent_shape[1:])
+        if self.ca:
+            t["ent_aux"] = cache[:, self.ce:]
+        return t
+
+    def _local_grads(self, batch, neg, is_train, optimizer, cache, gbufs, prof_events=None):
+        """kge_step (KGE_OPT_GRAD) on the cache; gbufs receive the cache's
+        duplicate-summed gradient rows."""
+        if self.fused is not None:
+            f = self.fused
+            f.tables = self._local_tables(cache)
+            grads = [gbufs[0], self.grel["rel"]]
+            if "rel_aux" in self.grel:
+                grads.append(self.grel["rel_aux"])
+            if self.ca:
+                grads.append(gbufs[1])
+            f.grads = grads
+            f(batch, is_train, optimizer if is_train else None, neg_ids=neg, prof_events=prof_events)
             return
         # host-only (KGE_BACKEND=eager) restatement of the same phase, for the gloo tests
-        loss, grads = engine.eager_grads(self.model, batch, is_train, neg=self._neg_triples(batch, neg_ids),
-                                         batch_scale=float(self.ex.world))
+        m = self.model
+        saved = dict(m.model_weights)
+        lt = self._local_tables(cache)
+        try:
+            m.model_weights[self.names["ent"]] = lt["ent"]
+            if self.ca:
+                m.model_weights[self.names["ent_aux"]] = lt["ent_aux"]
+            loss, grads = engine.eager_grads(m, batch, is_train, neg=self._neg_triples(batch, neg),
+                                             batch_scale=float(self.G))
+        finally:
+            m.model_weights.update(saved)
         self.red.zero_()
-        self.gfull.zero_()
+        for b in gbufs:
+            b.zero_()
         self.loss.fill_(float(loss))
-        for v, role in enumerate(("ent", "rel")):
-            name = self.names[role]
-            g = grads.get(name)
+        slot = {"ent": 0, "rel": 1, "rel_aux": 2, "ent_aux": 3}
+        for role in ("ent", "ent_aux", "rel", "rel_aux"):
+            name = self.names.get(role)
+            g = grads.get(name) if name else None
             if g is None:
                 continue
-            self.norm2[v] = engine.grad_norm2(g)
-            w = self.model.model_weights[name]
+            self.norm2[slot[role]] = engine.grad_norm2(g)
+            w = lt[role] if role in ("ent", "ent_aux") else m.model_weights[name]
             dg = engine.dense_grad(g, w).reshape(w.shape[0], -1)
-            (self.gfull[:self.E] if role == "ent" else self.grel).copy_(dg)
+            if role == "ent":
+                gbufs[0].copy_(dg)
+            elif role == "ent_aux":
+                gbufs[1].copy_(dg)
+            else:
+                self.grel[role].copy_(dg)
 
     def _neg_triples(self, batch, neg_ids):
         m = self.model
-        if neg_ids is None:
-            return None
         K = int(m.negative_ratio)
         if m.corrupt_side == "h+t":
             K = 2 * (K // 2)
@@ -171,45 +314,140 @@ class ShardedStep:
             rep[1::2, 2] = neg_ids[1::2]
         return rep
 
-    def _apply(self, optimizer):
-        rel = self.model.model_weights[self.names["rel"]]
-        if isinstance(optimizer, _opt.Adam):
-            optimizer.iterations += 1
-        pairs = [(self.shard[:self.valid], self.gshard[:self.valid], 0, self.names["ent"] + "#shard"),
-                 (rel.view(rel.shape[0], -1), self.grel, 1, self.names["rel"])]
-        for var, grad, v, name in pairs:
-            if var.shape[0] == 0:
-                continue
-            if self.fused is not None:
-                self.fused.apply(var, grad, self.norm2.data_ptr() + 4 * v, optimizer, name)
+    def _slot(self, k):
+        """norm2 slot of entity table k (0 ent_emb, 3 ent_proj)."""
+        return 0 if k == 0 else 3
+
+    def _apply_sparse(self, optimizer, gbufs, sc, rc, rids):
+        """Gradient rows back to their owners, owner-side sum + apply."""
+        G, ex = self.G, self.ex
+        n_in = sum(rc)
+        U = gbufs[0].shape[0]
+        lidx = torch.div(rids, G, rounding_mode="floor")
+        touched = torch.unique(lidx)
+        pos = torch.searchsorted(touched, lidx)
+        bounds = [0]
+        for c in rc:
+            bounds.append(bounds[-1] + c)
+        adam = isinstance(optimizer, _opt.Adam)
+        for k, gb in enumerate(gbufs):
+            cols = gb.shape[1]
+            back = torch.empty(n_in, cols, dtype=torch.float32, device=gb.device)
+            ex.all_to_all(back, gb[:U].contiguous(), rc, sc)
+            # each source's rows are unique: index_add_ per source is collision-free
+            acc = torch.zeros(touched.shape[0] if not adam else self.Es, cols, dtype=torch.float32,
+                              device=gb.device)
+            tgt = pos if not adam else lidx
+            for s in range(G):
+                a, b = bounds[s], bounds[s + 1]
+                if b > a:
+                    acc.index_add_(0, tgt[a:b], back[a:b])
+            lo = 0 if k == 0 else self.ce
+            var = self.shard[:, lo:lo + cols]
+            v = self._slot(k)
+            if adam:
+                self._apply_dense(var[:self.valid], acc[:self.valid], v, optimizer, self._shard_name(k))
+            elif self.fused is not None:
+                a = _hip.kge_apply_rows_desc()
+                a.var = _hip.table(var)
+                a.rows = touched.data_ptr()
+                a.n = int(touched.shape[0])
+                a.grad = acc.data_ptr()
+                a.grad_ld = cols
+                a.norm2 = self.norm2.data_ptr() + 4 * v
+                a.lr = optimizer.learning_rate
+                a.clip_norm = 5.0
+                _hip.check(self.lib.kge_apply_rows(ctypes.byref(a), _hip.stream_handle(var.device)), "kge_apply_rows")
             else:
-                _host_apply(var, grad, self.norm2[v], optimizer, name)
+                with torch.no_grad():
+                    cs = 5.0 / max(math.sqrt(float(self.norm2[v])), 5.0)
+                    var[touched] = var[touched] + (acc * cs) * (-optimizer.learning_rate)
+
+    def _shard_name(self, k):
+        return self.names["ent" if k == 0 else "ent_aux"] + "#shard"
+
+    def _apply_dense(self, var, grad, v, optimizer, name):
+        if var.shape[0] == 0:
+            return
+        if self.fused is not None:
+            self.fused.apply(var, grad, self.norm2.data_ptr() + 4 * v, optimizer, name)
+        else:
+            _host_apply(var, grad, self.norm2[v], optimizer, name)
+
+    def _apply_rel(self, optimizer):
+        slot = {"rel": 1, "rel_aux": 2}
+        for r in self.rel_roles:
+            w = self.tables[r]
+            self._apply_dense(w.view(w.shape[0], -1), self.grel[r], slot[r], optimizer, self.names[r])
 
     # ------------------------------------------------------------ step
     def __call__(self, batch, is_train, optimizer, neg_ids=None, prof_events=None):
-        self._constrain_shard()
-        self.ex.all_gather(self.full, self.shard)
-        self._local_grads(batch, is_train, neg_ids, optimizer, prof_events)
+        if isinstance(optimizer, _opt.Adam) and is_train:
+            optimizer.iterations += 1
+        self._constrain()
+        if neg_ids is None:
+            neg_ids = self._draw(batch)
+        Bn = int(batch.shape[0])
+        ids = torch.cat([batch[:, 0], batch[:, 2], neg_ids.to(batch.dtype)]).to(torch.int64)
+        if self.mode == "sparse":
+            cache, remap, plan = self._fetch_sparse(ids)
+            gbufs = [b[:cache.shape[0]] for b in self._gcache] if self.fused is not None else \
+                [torch.zeros(cache.shape[0], c) for c in self._ecols()]
+        else:
+            self.ex.all_gather(self.full, self.shard)
+            cache = self.full
+            G, Es = self.G, self.Es
+            remap = (ids % G) * Es + torch.div(ids, G, rounding_mode="floor")
+            gbufs = self.gfull
+        lb = batch.clone()
+        lb[:, 0] = remap[:Bn].to(batch.dtype)
+        lb[:, 2] = remap[Bn:2 * Bn].to(batch.dtype)
+        lneg = remap[2 * Bn:].to(batch.dtype).contiguous()
+        self._local_grads(lb, lneg, is_train, optimizer, cache, gbufs, prof_events)
         self.ex.all_reduce(self.red)
         if is_train:
-            self.ex.reduce_scatter(self.gshard, self.gfull)
-            self._apply(optimizer)
+            if self.mode == "sparse":
+                self._apply_sparse(optimizer, gbufs, *plan)
+            else:
+                for k in range(len(gbufs)):
+                    self.ex.reduce_scatter(self.gshard[k], self.gfull[k])
+                    lo = 0 if k == 0 else self.ce
+                    var = self.shard[:self.valid, lo:lo + gbufs[k].shape[1]]
+                    self._apply_dense(var, self.gshard[k][:self.valid], self._slot(k), optimizer, self._shard_name(k))
+            self._apply_rel(optimizer)
         return self.loss
 
+    # ------------------------------------------------------------ state
     def sync(self):
-        """Gather the current shards so ``model_weights`` is up to date (evaluation)."""
-        self.ex.all_gather(self.full, self.shard)
+        """Gather the shards into ``model_weights`` in id order (evaluation,
+        checkpoints)."""
+        G, Es = self.G, self.Es
+        full = torch.zeros(G * Es, self.C, dtype=torch.float32, device=self.device)
+        self.ex.all_gather(full, self.shard)
+        nat = full.view(G, Es, self.C).transpose(0, 1).reshape(G * Es, self.C)[:self.E]
+        w = self.model.model_weights
+        with torch.no_grad():
+            w[self.names["ent"]].copy_(nat[:, :self.ce].reshape(self.ent_shape))
+            if self.ca:
+                w[self.names["ent_aux"]].copy_(nat[:, self.ce:].reshape(self.aux_shape))
+
+    def load(self, weights):
+        """Write ``weights`` (id order) into this rank's shard and the
+        replicated tables (checkpoint restore)."""
+        G, g = self.G, self.g
+        with torch.no_grad():
+            ent = torch.as_tensor(weights[self.names["ent"]]).to(self.device).reshape(self.E, -1)
+            self.shard[:self.valid, :self.ce] = ent[g::G]
+            if self.ca:
+                aux = torch.as_tensor(weights[self.names["ent_aux"]]).to(self.device).reshape(self.E, -1)
+                self.shard[:self.valid, self.ce:] = aux[g::G]
+            for r in self.rel_roles:
+                self.tables[r].copy_(torch.as_tensor(weights[self.names[r]]).to(self.device))
+        self.sync()
 
     def check_status(self):
         if self.fused is not None:
-            self.fused.check_status()
-
-
-def _rel_name(model):
-    for k in ("rel_emb", "rel_inter"):
-        if k in model.model_weights:
-            return k
-    raise ValueError("no relation table")
+            _hip.check_device_status(self.status, "kge_step")
 
 
 def _host_apply(var, grad, norm2, optimizer, name):

@@ -405,9 +405,38 @@ __global__ __launch_bounds__(256) void apply_kernel(float* __restrict__ w, int64
   }
 }
 
+// rows[i] of var += -lr * clip * g[i]: one wave per listed row
+__global__ __launch_bounds__(256) void apply_rows_kernel(float* __restrict__ w, int64_t ld, int32_t cols,
+                                                          const int64_t* __restrict__ rows, int64_t n,
+                                                          const float* __restrict__ g, int64_t gld,
+                                                          const float* __restrict__ norm2, float lr, float clip) {
+  const float cs = clip / fmaxf(sqrtf(*norm2), clip);
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x / KGE_WAVE);
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x / KGE_WAVE) + wave_id(); i < n; i += nw) {
+    float* wr = w + rows[i] * ld;
+    const float* gr = g + i * gld;
+    for (int c = lane_id(); c < cols; c += KGE_WAVE) wr[c] = wr[c] + (gr[c] * cs) * (-lr);
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+kge_status kge_apply_rows(const kge_apply_rows_desc* d, void* stream) {
+  if (!d) return fail(KGE_EINVAL, "null descriptor");
+  const kge_table& t = d->var;
+  if (!t.data || t.rows < 0 || t.cols <= 0 || t.ld < t.cols) return fail(KGE_EINVAL, "kge_apply_rows: bad table");
+  if (d->n < 0) return fail(KGE_EINVAL, "kge_apply_rows: n must be >= 0");
+  if (d->n == 0) return KGE_OK;
+  if (!d->rows || !d->grad || !d->norm2 || d->grad_ld < t.cols)
+    return fail(KGE_EINVAL, "kge_apply_rows: null rows / grad / norm2 or grad_ld < cols");
+  if (!(d->clip_norm > 0.f)) return fail(KGE_EINVAL, "kge_apply_rows: clip_norm must be > 0");
+  const int64_t blocks = std::min<int64_t>(ceil_div(d->n, kWaves), 8192);
+  hipLaunchKernelGGL(apply_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, t.data, t.ld,
+                     (int32_t)t.cols, d->rows, d->n, d->grad, d->grad_ld, d->norm2, d->lr, d->clip_norm);
+  return hip_check("kge_apply_rows");
+}
 
 kge_status kge_apply(const kge_apply_desc* d, void* stream) {
   if (!d) return fail(KGE_EINVAL, "null descriptor");

@@ -559,9 +559,15 @@ def test_fused_adam_first_step(hiplib, model_name):
     check(ref, got, l_, ps, ns)
 
 
-def test_sharded_step_world1_rccl(hiplib):
-    """KGE/sharded.py on the RCCL backend (world size 1): shard, all-gather,
-    grad-mode kge_step, all-reduce, reduce-scatter, kge_apply == the oracle step."""
+@pytest.mark.parametrize("mode", ["sparse", "dense"])
+@pytest.mark.parametrize("model_name,score_kind", [("TransE", "lp2"), ("TransD", "lppow2"), ("RotatE", "lp1"),
+                                                   ("TransR", "lppow2"), ("DistMult", None)])
+def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
+    """KGE/sharded.py on the RCCL backend (world size 1): e mod G shard,
+    kge_sample draws, the sparse (unique ids -> all_to_all ids / rows -> row
+    cache -> gradient rows back -> kge_apply_rows) or dense (all-gather /
+    reduce-scatter) exchange, grad-mode kge_step on the cache, all-reduce,
+    two steps == two oracle steps with the same draws."""
     import socket
     import torch.distributed as dist
     from KGE import loss, optimizers, score
@@ -576,22 +582,79 @@ def test_sharded_step_world1_rccl(hiplib):
                             device_id=dev)
     try:
         rng = np.random.default_rng(3)
-        E, R, d, B, K = 37, 5, 64, 16, 8
-        W = _weights("TransE", E, R, d, rng)
-        pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
-        m = _make("TransE", d, K, "h+t", score.LpDistance(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
-                  E, R, UniformStrategy(np.arange(E), seed=9))
-        m.model_weights = {k: torch.tensor(v, device=dev) for k, v in W.items()}
-        st = ShardedStep(m)
-        plane = m.ns_strategy.offset
-        lv = float(st(torch.tensor(pos, device=dev), True, optimizers.SGD(0.05)))
-        torch.cuda.synchronize()
-        st.check_status()
+        E, R, d, B, K = 37, 5, 24, 16, 8
+        k = 20 if model_name in ("TransD", "TransR") else None
+        W = _weights(model_name, E, R, d, rng, k)
+        sc = {"lp2": score.LpDistance(2), "lppow2": score.LpDistancePow(2), "lp1": score.LpDistance(1),
+              None: None}[score_kind]
+        m = _make(model_name, d, K, "h+t", sc, loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E, R,
+                  UniformStrategy(np.arange(E), seed=9), k=k)
+        m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
+        st = ShardedStep(m, mode=mode)
+        ref_w = W
+        opt = optimizers.SGD(0.05)
+        for it in range(2):
+            pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+            plane = m.ns_strategy.offset
+            lv = float(st(torch.tensor(pos, device=dev), True, opt))
+            torch.cuda.synchronize()
+            st.check_status()
+            neg = orc.negatives(pos, K, "h+t", E, seed=9, plane=plane)
+            ref = orc.train_step(model_name, ref_w, pos, neg, score=_spec_score(sc) if sc is not None else ("dot", 0.0),
+                                 loss=("sans", 3.0, 1.0), lr=0.05, limit=getattr(m, "limit", None),
+                                 constraint=model_name != "RotatE",
+                                 constraint_weight=getattr(m, "constraint_weight", 1.0))
+            ref_w = ref["weights"]
+            assert abs(lv - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"])), it
         st.sync()
-        neg = orc.negatives(pos, K, "h+t", E, seed=9, plane=plane)
-        ref = orc.train_step("TransE", W, pos, neg, score=("lp", 2.0), loss=("sans", 3.0, 1.0), lr=0.05)
-        assert abs(lv - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"]))
-        for k, v in ref["weights"].items():
-            np.testing.assert_allclose(m.model_weights[k].cpu().numpy(), v, atol=TOL, err_msg=k)
+        for kk, v in ref_w.items():
+            np.testing.assert_allclose(m.model_weights[kk].cpu().numpy(), v, atol=TOL, err_msg=kk)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_step_c5_shard_size(hiplib):
+    """One GPU at the C5 per-rank shard size (6.25M rows x 512, TransE, K=256
+    h+t, SANS) through the sparse exchange: finite loss, only touched rows
+    change, and the owner update equals the fused single-device step on the
+    same rows (same draws)."""
+    import socket
+    import torch.distributed as dist
+    from KGE import engine, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    from KGE.sharded import ShardedStep
+    dev = _dev()
+    s_ = socket.socket()
+    s_.bind(("127.0.0.1", 0))
+    port = s_.getsockname()[1]
+    s_.close()
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        E, R, d, B, K = 6_250_000, 1000, 512, 256, 256
+        g = torch.Generator(device=dev).manual_seed(0)
+        ent = (torch.rand(E, d, generator=g, device=dev) - 0.5) * 0.1
+        rel = (torch.rand(R, d, generator=g, device=dev) - 0.5) * 0.1
+        pos = torch.stack([torch.randint(0, E, (B,), generator=g, device=dev),
+                           torch.randint(0, R, (B,), generator=g, device=dev),
+                           torch.randint(0, E, (B,), generator=g, device=dev)], 1)
+        outs = []
+        for sharded in (True, False):
+            m = _make("TransE", d, K, "h+t", score.LpDistance(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
+                      E, R, UniformStrategy(np.arange(E), seed=5), constraint=False)
+            m.model_weights = {"ent_emb": ent.clone(), "rel_emb": rel.clone()}
+            stp = ShardedStep(m, mode="sparse") if sharded else engine.FusedStep(m)
+            lv = float(stp(pos, True, optimizers.SGD(0.01)))
+            torch.cuda.synchronize()
+            stp.check_status()
+            if sharded:
+                stp.sync()
+            outs.append((lv, m.model_weights["ent_emb"], m.model_weights["rel_emb"]))
+            del stp
+        assert math.isfinite(outs[0][0]) and abs(outs[0][0] - outs[1][0]) <= 1e-5 * max(1.0, abs(outs[1][0]))
+        changed = (outs[0][1] != ent).any(dim=1)
+        assert 0 < int(changed.sum()) <= B * (K + 2)
+        assert float((outs[0][1] - outs[1][1]).abs().max()) <= 1e-5
+        assert float((outs[0][2] - outs[1][2]).abs().max()) <= 1e-5
     finally:
         dist.destroy_process_group()

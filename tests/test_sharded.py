@@ -1,6 +1,8 @@
-"""CPU (gloo, world size 2): the multi-GPU step's exchange logic
-(KGE/sharded.py) -- row-sharded entity table, all-gather, global-batch loss
-normalisation, reduce-scatter, global clip norm, sharded apply -- gives the
+"""CPU (gloo, world size 2): the multi-GPU step (KGE/sharded.py) -- e mod G
+row ownership, negatives per rank, the sparse exchange (unique ids ->
+all_to_all of ids and rows -> local row cache -> gradient rows back ->
+owner-side sum + apply) and the dense one (all-gather / reduce-scatter),
+global-batch loss normalisation, global clip norm -- gives the
 single-device step on the concatenated batch. The local gradient phase runs
 the host restatement (KGE_BACKEND=eager); on GPUs it is kge_step."""
 
@@ -14,7 +16,7 @@ import torch.multiprocessing as mp
 
 from oracle import kge_oracle as orc
 
-E, R, D, B, K = 13, 4, 8, 5, 4   # E odd: the last shard is padded
+E, R, D, B, K = 13, 4, 8, 5, 4   # E odd: ranks own 7 and 6 rows
 
 
 def _port():
@@ -29,16 +31,25 @@ def _model(name, W, loss):
     from KGE import loss as L
     from KGE import score
     from KGE.models.semantic_based.DistMult import DistMult
+    from KGE.models.translating_based.RotatE import RotatE
+    from KGE.models.translating_based.TransD import TransD
     from KGE.models.translating_based.TransE import TransE
     from KGE.ns_strategy import UniformStrategy
     lf = {"sans": L.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), "hinge": L.PairwiseHingeLoss(1.0),
           "bce": L.BinaryCrossEntropyLoss()}[loss]
+    ns = UniformStrategy(np.arange(E), seed=1)
     if name == "TransE":
-        m = TransE({"embedding_size": D}, K, "h+t", score_fn=score.LpDistance(2), loss_fn=lf,
-                   ns_strategy=UniformStrategy(np.arange(E), seed=1), constraint=True)
+        m = TransE({"embedding_size": D}, K, "h+t", score_fn=score.LpDistance(2), loss_fn=lf, ns_strategy=ns,
+                   constraint=True)
+    elif name == "TransD":
+        m = TransD({"ent_embedding_size": D, "rel_embedding_size": 6}, K, "h+t", score_fn=score.LpDistancePow(2),
+                   loss_fn=lf, ns_strategy=ns, constraint=True)
+    elif name == "RotatE":
+        m = RotatE({"embedding_size": D}, K, "h+t", score_fn=score.LpDistance(1), loss_fn=lf, ns_strategy=ns)
+        m.limit = 0.7
     else:
-        m = DistMult({"embedding_size": D}, K, "h+t", loss_fn=lf, ns_strategy=UniformStrategy(np.arange(E), seed=1),
-                     constraint=True, constraint_weight=0.1)
+        m = DistMult({"embedding_size": D}, K, "h+t", loss_fn=lf, ns_strategy=ns, constraint=True,
+                     constraint_weight=0.1)
     m.metadata = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
     m.model_weights = {k: torch.tensor(v, dtype=torch.float32) for k, v in W.items()}
     return m
@@ -46,14 +57,20 @@ def _model(name, W, loss):
 
 def _case(seed, name):
     rng = np.random.default_rng(seed)
-    rk = "rel_emb" if name == "TransE" else "rel_inter"
-    W = {"ent_emb": rng.uniform(-0.5, 0.5, (E, D)), rk: rng.uniform(-0.5, 0.5, (R, D))}
+    if name == "TransD":
+        W = {"ent_emb": rng.uniform(-0.5, 0.5, (E, D)), "rel_emb": rng.uniform(-0.5, 0.5, (R, 6)),
+             "ent_proj": rng.uniform(-0.5, 0.5, (E, D)), "rel_proj": rng.uniform(-0.5, 0.5, (R, 6))}
+    elif name == "RotatE":
+        W = {"ent_emb": rng.uniform(-0.5, 0.5, (E, D, 2)), "rel_emb": rng.uniform(-0.5, 0.5, (R, D))}
+    else:
+        rk = "rel_emb" if name == "TransE" else "rel_inter"
+        W = {"ent_emb": rng.uniform(-0.5, 0.5, (E, D)), rk: rng.uniform(-0.5, 0.5, (R, D))}
     pos = np.stack([rng.integers(0, E, 2 * B), rng.integers(0, R, 2 * B), rng.integers(0, E, 2 * B)], 1)
     neg = rng.integers(0, E, 2 * B * K)
     return W, pos, neg
 
 
-def _worker(rank, port, name, loss, opt, steps, out):
+def _worker(rank, port, name, loss, opt, steps, mode, out):
     os.environ["KGE_BACKEND"] = "eager"
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=2)
@@ -61,7 +78,8 @@ def _worker(rank, port, name, loss, opt, steps, out):
     from KGE.sharded import ShardedStep
     W, pos, neg = _case(0, name)
     m = _model(name, W, loss)
-    st = ShardedStep(m)
+    st = ShardedStep(m, mode=mode)
+    assert st.valid == len(range(rank, E, 2))
     o = optimizers.SGD(0.05) if opt == "sgd" else optimizers.Adam(0.01)
     for s in range(steps):
         b = torch.tensor(pos[rank * B:(rank + 1) * B])
@@ -74,11 +92,11 @@ def _worker(rank, port, name, loss, opt, steps, out):
     dist.destroy_process_group()
 
 
-def _run(name, loss, opt, steps):
+def _run(name, loss, opt, steps, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, port, name, loss, opt, steps, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, port, name, loss, opt, steps, mode, q)) for r in range(2)]
     for p in ps:
         p.start()
     res = q.get(timeout=240)
@@ -88,25 +106,28 @@ def _run(name, loss, opt, steps):
     return res
 
 
-@pytest.mark.parametrize("name,loss", [("TransE", "sans"), ("TransE", "hinge"), ("DistMult", "bce")])
-def test_sharded_sgd_equals_single_device_oracle(name, loss):
-    got, got_loss = _run(name, loss, "sgd", 1)
+@pytest.mark.parametrize("mode", ["sparse", "dense"])
+@pytest.mark.parametrize("name,loss", [("TransE", "sans"), ("TransE", "hinge"), ("DistMult", "bce"),
+                                       ("TransD", "hinge"), ("RotatE", "sans")])
+def test_sharded_sgd_equals_single_device_oracle(name, loss, mode):
+    got, got_loss = _run(name, loss, "sgd", 1, mode)
     W, pos, neg = _case(0, name)
     spec = {"sans": ("sans", 3.0, 1.0), "hinge": ("hinge", 1.0), "bce": ("bce",)}[loss]
-    sc = ("lp", 2.0) if name == "TransE" else ("dot", 0.0)
-    ref = orc.train_step(name, W, pos, neg, score=sc, loss=spec, lr=0.05, constraint=True,
-                         constraint_weight=0.1, side="h+t")
+    sc = {"TransE": ("lp", 2.0), "DistMult": ("dot", 0.0), "TransD": ("lppow", 2.0), "RotatE": ("lp", 1.0)}[name]
+    ref = orc.train_step(name, W, pos, neg, score=sc, loss=spec, lr=0.05, constraint=name != "RotatE",
+                         constraint_weight=0.1, side="h+t", limit=0.7)
     assert abs(got_loss - ref["loss"]) <= 1e-5 * max(1.0, abs(ref["loss"]))
     for k, v in ref["weights"].items():
         np.testing.assert_allclose(got[k], v, atol=2e-6, err_msg=k)
 
 
-def test_sharded_adam_equals_single_device_eager():
+@pytest.mark.parametrize("mode", ["sparse", "dense"])
+def test_sharded_adam_equals_single_device_eager(mode):
     """Two Adam steps across 2 ranks == two steps of the single-process eager path at 2B."""
     os.environ["KGE_BACKEND"] = "eager"
     try:
         from KGE import engine, optimizers
-        got, _ = _run("TransE", "sans", "adam", 2)
+        got, _ = _run("TransE", "sans", "adam", 2, mode)
         W, pos, neg = _case(0, "TransE")
         m = _model("TransE", W, "sans")
         o = optimizers.Adam(0.01)
