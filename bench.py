@@ -14,6 +14,9 @@ Other legs (``--workload``; one JSON line each, same schema):
   c4-rescal  RESCAL d=200, B=512, K=64, SquareError, constraint (dense regulariser)
   c4-transr  TransR d=k=200, B=512, K=64, LpDistancePow(2), hinge(1), constraint (fp32 MFMA)
   c2-50m     the C2 step on a synthetic 50M-entity table (HBM-honest point; SURVEY 8(d) Caveat)
+  c5         TransE d=512 on a synthetic 50M-entity / 1000-relation graph with Zipf(1.1) heads /
+             tails and Zipf(1.2) relations, entity table row-sharded (e mod N)
+             through KGE/sharded.py's sparse all-to-all exchange at every N (N = 1 included)
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 one process per GPU, each with its own 1024-positive batch (weak scaling, the
@@ -44,7 +47,7 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 F32_MFMA_PEAK_TF = 157.3   # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
 
-WORKLOADS = ("c2", "c1", "c3", "c4-rescal", "c4-transr", "c2-50m")
+WORKLOADS = ("c2", "c1", "c3", "c4-rescal", "c4-transr", "c2-50m", "c5")
 
 
 def parse():
@@ -97,6 +100,14 @@ def spec(name, args):
                        desc="C2 step on a synthetic %(E)d-entity table: TransE d=%(d)d, batch=%(B)d, %(K)d negs h+t, "
                             "SANS(3,1), LpDistance(2), uniform ids, no constraint (a full-table renormalisation "
                             "would be an 80 GB pass per step), SGD"),
+        "c5": dict(model="TransE", B=1024, K=256, d=512, side="h+t", constraint=False,
+                   score=score.LpDistance(p=2),
+                   loss=loss.SelfAdversarialNegativeSamplingLoss(margin=3, temperature=1), E=50_000_000, R=1000,
+                   zipf=True, sharded=True,
+                   desc="C5: TransE d=%(d)d on a synthetic %(E)d-entity graph (Zipf(1.1) heads/tails, Zipf(1.2) "
+                        "relations, R=1000), batch=%(B)d per GPU, %(K)d negs h+t, SANS(3,1), LpDistance(2), "
+                        "uniform negatives, no constraint, SGD; entity rows sharded e mod N, sparse all-to-all "
+                        "exchange"),
     }[name]
     if args.batch:
         w["B"] = args.batch
@@ -105,6 +116,18 @@ def spec(name, args):
     if args.dim:
         w["d"] = args.dim
     return w
+
+
+def zipf_ids(n, N, s, g, dev):
+    """Truncated power-law ranks k in [1, N] (inverse CDF of the continuous
+    Zipf(s) density) mapped through the bijection k -> (a (k-1) + b) mod N,
+    a coprime to N: heavy hitters scattered over the id space."""
+    u = torch.rand(n, generator=g, device=dev, dtype=torch.float64)
+    k = torch.pow(1.0 + u * (float(N) ** (1.0 - s) - 1.0), 1.0 / (1.0 - s)).floor().clamp_(1, N).to(torch.int64)
+    a = 2654435761
+    while np.gcd(a, N) != 1:
+        a += 2
+    return (a * (k - 1) + 40503) % N
 
 
 def build_model(w, E, R, rank, dev):
@@ -255,17 +278,35 @@ def main():
     synthetic = "E" in w
     if synthetic:
         E = w["E"]
+        R = w.get("R", R)
     B, K, d = w["B"], w["K"], w["d"]
+    sharded = world > 1 or w.get("sharded", False)
+    if sharded and world == 1:
+        # one-rank process group: the same sharded step (and its exchange) as at N > 1
+        import socket
+        import torch.distributed as dist
+        s_ = socket.socket()
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+        s_.close()
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
+                                device_id=dev)
     model, opt = build_model(w, E, R, rank, dev)
-    if world > 1:
+    if sharded:
         from KGE.sharded import ShardedStep
-        step = ShardedStep(model)
+        step = ShardedStep(model, mode="sparse" if w.get("sharded") else "auto")
+        if E > 10_000_000:
+            step.release_entity_tables()   # the shard is the only copy the step needs
     else:
         step = engine.FusedStep(model)
 
     # batches resident in HBM before timing: a shuffled stream per rank
     nb = args.warmup + args.steps
-    if synthetic:
+    if w.get("zipf"):
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        batches = torch.stack([zipf_ids(nb * B, E, 1.1, g, dev), zipf_ids(nb * B, R, 1.2, g, dev),
+                               zipf_ids(nb * B, E, 1.1, g, dev)], -1).reshape(nb, B, 3).contiguous()
+    elif synthetic:
         g = torch.Generator(device=dev).manual_seed(1000 + rank)
         batches = torch.stack([torch.randint(0, E, (nb, B), generator=g, device=dev),
                                torch.randint(0, R, (nb, B), generator=g, device=dev),
@@ -312,7 +353,7 @@ def main():
     k0 = float(np.mean([r[0].elapsed_time(r[1]) for r in evs]))
     ks = float(np.mean([r[1].elapsed_time(r[2]) for r in evs]))
     ku = float(np.mean([r[2].elapsed_time(r[3]) for r in evs]))
-    if world > 1:
+    if sharded:
         t = torch.tensor([ms], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         ms = float(t.item())
@@ -363,15 +404,18 @@ def main():
         "value": round(value, 1), "unit": "positive-triples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32",
-        "data": ("synthetic uniform ids over %d entities / %d relations; random-init weights" % (E, R)) if synthetic
+        "data": ("synthetic %s ids over %d entities / %d relations; random-init weights"
+                 % ("Zipf" if w.get("zipf") else "uniform", E, R)) if synthetic
         else "FB15k-237 train_indexed ids (real graph); random-init weights",
         "config": {"workload": w["desc"] % dict(B=B, K=K, d=d, E=E), "global_batch": world * B,
                    "negatives": K, "dim": d, "parallelism": "dp%d" % world,
                    "scored_triples_per_s": round(value * (1 + K), 1)},
         "roofline": roof, "cpu_baseline": cpu,
     }
+    if sharded:
+        out["config"]["exchange"] = step.mode
     print(json.dumps(out))
-    if world > 1:
+    if sharded:
         torch.distributed.destroy_process_group()
 
 

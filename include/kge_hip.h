@@ -104,8 +104,11 @@ enum {
                                        _constraint_loss assigns (e.g. on its shard) */
   KGE_FLAG_DEBUG_LIST_CAP = 2,      /* test hook: 4-entry destination lists, so the
                                        update kernel's overflow path runs */
-  KGE_FLAG_DEBUG_UNFUSED_CONSTRAINT = 4 /* test hook: run the full-table renormalisation
+  KGE_FLAG_DEBUG_UNFUSED_CONSTRAINT = 4, /* test hook: run the full-table renormalisation
                                        as its own kernel even on the SGD path */
+  KGE_FLAG_GRAD_ROWS_TOUCHED = 8     /* KGE_OPT_GRAD: the caller needs only the entity
+                                       gradient rows the batch touches (a row cache of
+                                       exactly the batch's ids): no zero-fill of grad_out[0/3] */
 };
 
 typedef struct kge_table {

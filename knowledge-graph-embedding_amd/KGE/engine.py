@@ -277,6 +277,10 @@ class FusedStep:
                 # zero-filled once: the step's tickets / destination counters
                 # live in the workspace and reset themselves between calls
                 self.workspace = torch.zeros(need, dtype=torch.uint8, device=self.device)
+            elif cached is not None:
+                # a different plan lays the workspace out differently: its
+                # counters must start from zeros again
+                self.workspace.zero_()
             d.workspace = self.workspace.data_ptr()
             d.workspace_bytes = self.workspace.numel()
             self._cache = (key, d)

@@ -153,6 +153,8 @@ class ShardedStep:
             f.status = self.status
             f.batch_scale = float(G)
             f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT
+            if mode == "sparse":   # every cache row [0, U) is a batch id: no gradient zero-fill
+                f.flags |= _hip.FLAG_GRAD_ROWS_TOUCHED
             self.fused = f
         elif engine.backend() != "eager":
             raise RuntimeError("ShardedStep needs GPUs (or KGE_BACKEND=eager for host-only tests)")
@@ -229,18 +231,23 @@ class ShardedStep:
         rows = self.shard[torch.div(rids, G, rounding_mode="floor")]
         U = int(req.shape[0])
         cache = self._cache_buf(U)
-        ex.all_to_all(cache, rows, sc, rc)
+        ex.all_to_all(cache[:U], rows, sc, rc)
         inv = torch.empty_like(order)
         inv[order] = torch.arange(U, device=order.device)
         remap = inv[torch.searchsorted(uniq, ids)]
         return cache, remap, (sc, rc, rids)
 
     def _cache_buf(self, U):
+        """The row cache at a FIXED capacity (the kernel's table shape, hence
+        its plan and workspace layout, stays the same from step to step):
+        rows [0, U) hold this step's unique rows, the rest are never referenced."""
         if U > self._cap:
-            self._cap = max(U, int(self._cap * 1.25))
-            self._cache = torch.empty(self._cap, self.C, dtype=torch.float32, device=self.device)
-            self._gcache = [torch.empty(self._cap, c, dtype=torch.float32, device=self.device) for c in self._ecols()]
-        return self._cache[:U]
+            m = self.model
+            keff = 2 * (int(m.negative_ratio) // 2) if m.corrupt_side == "h+t" else int(m.negative_ratio)
+            self._cap = max(U, min(self.E, self._bmax * (keff + 2)))
+            self._cache = torch.zeros(self._cap, self.C, dtype=torch.float32, device=self.device)
+            self._gcache = [torch.zeros(self._cap, c, dtype=torch.float32, device=self.device) for c in self._ecols()]
+        return self._cache
 
     def _local_tables(self, cache):
         """The model's tables with the entity tables replaced by cache views."""
@@ -322,7 +329,7 @@ class ShardedStep:
         """Gradient rows back to their owners, owner-side sum + apply."""
         G, ex = self.G, self.ex
         n_in = sum(rc)
-        U = gbufs[0].shape[0]
+        U = sum(sc)            # this rank's unique rows = its cache rows [0, U)
         lidx = torch.div(rids, G, rounding_mode="floor")
         touched = torch.unique(lidx)
         pos = torch.searchsorted(touched, lidx)
@@ -390,9 +397,9 @@ class ShardedStep:
         Bn = int(batch.shape[0])
         ids = torch.cat([batch[:, 0], batch[:, 2], neg_ids.to(batch.dtype)]).to(torch.int64)
         if self.mode == "sparse":
+            self._bmax = max(getattr(self, "_bmax", 0), Bn)
             cache, remap, plan = self._fetch_sparse(ids)
-            gbufs = [b[:cache.shape[0]] for b in self._gcache] if self.fused is not None else \
-                [torch.zeros(cache.shape[0], c) for c in self._ecols()]
+            gbufs = self._gcache if self.fused is not None else [torch.zeros(cache.shape[0], c) for c in self._ecols()]
         else:
             self.ex.all_gather(self.full, self.shard)
             cache = self.full
@@ -418,6 +425,17 @@ class ShardedStep:
         return self.loss
 
     # ------------------------------------------------------------ state
+    def release_entity_tables(self):
+        """Drop the id-order entity tables the model held (the shards are
+        authoritative; sync() allocates them again). Frees E x cols floats per
+        table on every rank -- needed when the table is most of HBM (C5)."""
+        w = self.model.model_weights
+        for role in ("ent", "ent_aux"):
+            if role in self.names and self.tables.get(role) is not None:
+                w[self.names[role]] = torch.empty(0, dtype=torch.float32, device=self.device)
+                self.tables[role] = self.tables[role][:0]
+        self._released = True
+
     def sync(self):
         """Gather the shards into ``model_weights`` in id order (evaluation,
         checkpoints)."""
@@ -426,6 +444,13 @@ class ShardedStep:
         self.ex.all_gather(full, self.shard)
         nat = full.view(G, Es, self.C).transpose(0, 1).reshape(G * Es, self.C)[:self.E]
         w = self.model.model_weights
+        if getattr(self, "_released", False):
+            w[self.names["ent"]] = torch.empty((self.E,) + self.ent_shape[1:], dtype=torch.float32,
+                                               device=self.device)
+            if self.ca:
+                w[self.names["ent_aux"]] = torch.empty((self.E,) + self.aux_shape[1:], dtype=torch.float32,
+                                                       device=self.device)
+            self._released = False
         with torch.no_grad():
             w[self.names["ent"]].copy_(nat[:, :self.ce].reshape(self.ent_shape))
             if self.ca:

@@ -574,12 +574,14 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   }
   hipEvent_t const* ev = (hipEvent_t const*)d->prof_events;
   if (ev) (void)hipEventRecord(ev[0], st);
+  const bool zero_ent = !(d->flags & KGE_FLAG_GRAD_ROWS_TOUCHED);
   if (A.grad_mode && !P.rescal) {   // RESCAL's dense passes write every row
-    (void)hipMemsetAsync(d->grad_out[0], 0, (size_t)A.ent.rows * A.ent.cols * sizeof(float), st);
+    if (zero_ent) (void)hipMemsetAsync(d->grad_out[0], 0, (size_t)A.ent.rows * A.ent.cols * sizeof(float), st);
     (void)hipMemsetAsync(d->grad_out[1], 0, (size_t)A.rel.rows * A.rel_gcols * sizeof(float), st);
     if (P.transr) (void)hipMemsetAsync(d->grad_out[2], 0, (size_t)TA.proj.rows * TA.proj.cols * sizeof(float), st);
     if (P.proj) (void)hipMemsetAsync(d->grad_out[2], 0, (size_t)d->rel_aux.rows * d->rel_aux.cols * sizeof(float), st);
-    if (P.td) (void)hipMemsetAsync(d->grad_out[3], 0, (size_t)d->ent_aux.rows * d->ent_aux.cols * sizeof(float), st);
+    if (P.td && zero_ent)
+      (void)hipMemsetAsync(d->grad_out[3], 0, (size_t)d->ent_aux.rows * d->ent_aux.cols * sizeof(float), st);
   }
   if (P.pj_dense && d->optimizer == KGE_OPT_SGD && d->batch > 0) {
     // the update passes write only the touched rows of the dense gradients
