@@ -11,6 +11,7 @@ constexpr int kUpdWaves = 4;       // waves per update workgroup (one destinatio
 constexpr int kUpdThreads = kUpdWaves * KGE_WAVE;
 constexpr int kMaxWpp = 8;         // waves per positive, at most
 constexpr int kMergeStride = 32;   // floats of per-positive merge state in the score kernel's LDS
+constexpr int kSortMax = 1024;     // update kernel: longest destination list sorted in LDS (per wave)
 
 // Control block at the head of the workspace. The caller zero-fills the
 // workspace once when it allocates it; every kernel that uses a word puts it

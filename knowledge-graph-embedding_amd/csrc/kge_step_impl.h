@@ -638,6 +638,7 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
   constexpr int RV = RelV<M::CPLX, VEC>::n;
   constexpr int CHMAX = 4;                            // in-register ordering up to 256 codes
   __shared__ uint32_t s_scr[kUpdWaves][CHMAX * KGE_WAVE];
+  __shared__ uint32_t s_sort[kUpdWaves][kSortMax];    // longer lists: gathered + bitonic-sorted here
 
   KGE_PROF_INIT();
   const int lane = lane_id(), wv = wave_id();
@@ -849,9 +850,51 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         consume_sorted([&](int p) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)scr[p]); });
+      } else if (n <= (uint32_t)kSortMax) {
+        // a long list (past its capacity or past 256 codes; skewed graphs):
+        // the list part and this destination's overflow entries (one pass
+        // over the overflow array, ballot-compacted) gathered into LDS, then
+        // a wave-local bitonic sort -- linear gather, n log^2 n compares
+        uint32_t* buf = s_sort[wv];
+        const uint32_t nl = min(n, (uint32_t)A.cap);
+        for (uint32_t q = lane; q < nl; q += KGE_WAVE) buf[q] = lst[q];
+        if (n > nl) {
+          const uint32_t novf = A.ctl->ovf_len;
+          uint32_t fill = nl;
+          for (uint32_t q0 = 0; q0 < novf && fill < n; q0 += KGE_WAVE) {
+            const uint32_t q = q0 + lane;
+            uint64_t y = 0;
+            const bool hit = q < novf && (int64_t)((y = A.ovf[q]) >> 32) == d;
+            const uint64_t m = __ballot(hit);
+            if (hit) buf[fill + __popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)y;
+            fill += (uint32_t)__popcll(m);
+          }
+        }
+        uint32_t P = 1;
+        while (P < n) P <<= 1;
+        for (uint32_t q = n + lane; q < P; q += KGE_WAVE) buf[q] = 0xFFFFFFFFu;
+        auto wave_sync = [] {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
+        wave_sync();
+        for (uint32_t k = 2; k <= P; k <<= 1) {
+          for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = lane; i < P; i += KGE_WAVE) {
+              const uint32_t l = i ^ j;
+              if (l > i) {
+                const uint32_t a = buf[i], b = buf[l];
+                if ((a > b) == ((i & k) == 0)) { buf[i] = b; buf[l] = a; }
+              }
+            }
+            wave_sync();
+          }
+        }
+        consume_sorted([&](int p) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)buf[p]); });
       } else {
-        // a list past its capacity: repeated selection of the next code from
-        // the list and the overflow entries (correct for any skew, not fast)
+        // past kSortMax codes: repeated selection of the next code from the
+        // list and the overflow entries (correct for any skew, not fast)
         const uint32_t nl = min(n, (uint32_t)A.cap);
         const uint32_t novf = A.ctl->ovf_len;
         uint32_t last = 0u;

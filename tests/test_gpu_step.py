@@ -445,6 +445,36 @@ def test_destination_list_overflow(hiplib, li):
     check(ref, got, l_, ps, ns)
 
 
+@pytest.mark.parametrize("model_name", ["TransE", "TransR", "TransD"])
+def test_zipf_skewed_batch(hiplib, model_name):
+    """Skewed keys (SURVEY 8(d) C5 shape): one entity takes 30% of the
+    negative draws (~600 keys for one destination), one relation 40% of the
+    positives -- lists far past their capacity go through the gather + LDS
+    bitonic-sort path of the update kernel; == the oracle."""
+    from KGE import engine, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    dev = _dev()
+    rng = np.random.default_rng(31)
+    E, R, d, B, K = 300, 6, 32, 64, 32
+    k = 24 if model_name in ("TransR", "TransD") else None
+    W = _weights(model_name, E, R, d, rng, k)
+    rels = np.where(rng.random(B) < 0.4, 2, rng.integers(0, R, B))
+    pos = np.stack([rng.integers(0, E, B), rels, rng.integers(0, E, B)], 1).astype(np.int64)
+    neg = np.where(rng.random(B * K) < 0.3, 7, rng.integers(0, E, B * K)).astype(np.int64)
+    sc = score.LpDistance(2) if model_name == "TransE" else score.LpDistancePow(2)
+    m = _make(model_name, d, K, "h+t", sc, loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E, R,
+              UniformStrategy(np.arange(E), seed=1), k=k)
+    m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
+    step = engine.FusedStep(m)
+    step(torch.tensor(pos, device=dev), True, optimizers.SGD(0.05), neg_ids=torch.tensor(neg, device=dev))
+    torch.cuda.synchronize()
+    step.check_status()
+    ref = orc.train_step(model_name, W, pos, neg, score=_spec_score(sc), loss=("sans", 3.0, 1.0), lr=0.05)
+    assert abs(float(step.loss_out.item()) - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"]))
+    for kk, v in ref["weights"].items():
+        np.testing.assert_allclose(m.model_weights[kk].cpu().numpy(), v, atol=TOL, err_msg=kk)
+
+
 def test_consecutive_steps_reuse_workspace(hiplib):
     """Three steps through one FusedStep (one workspace: tickets, list counters
     and the overflow counter must reset themselves) == three oracle steps."""
