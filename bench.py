@@ -42,6 +42,9 @@ for p in (ROOT, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# RCCL's version banner goes to stdout; the contract is ONE JSON line there
+os.environ["NCCL_DEBUG"] = "WARN"
+
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -61,6 +64,8 @@ def parse():
     ap.add_argument("--dim", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="c5 at one GPU: run the all-to-all exchange + row cache instead of the one-rank shortcut")
     return ap.parse_args()
 
 
@@ -294,7 +299,8 @@ def main():
     model, opt = build_model(w, E, R, rank, dev)
     if sharded:
         from KGE.sharded import ShardedStep
-        step = ShardedStep(model, mode="sparse" if w.get("sharded") else "auto")
+        step = ShardedStep(model, mode="sparse" if w.get("sharded") else "auto",
+                           local_fast=not args.force_exchange)
         if E > 10_000_000:
             step.release_entity_tables()   # the shard is the only copy the step needs
     else:
@@ -413,7 +419,8 @@ def main():
         "roofline": roof, "cpu_baseline": cpu,
     }
     if sharded:
-        out["config"]["exchange"] = step.mode
+        out["config"]["exchange"] = "local (one rank: fused step on the shard)" if step.direct is not None \
+            else step.mode
     print(json.dumps(out))
     if sharded:
         torch.distributed.destroy_process_group()

@@ -149,6 +149,7 @@ class FusedStep:
         self.batch_scale = 1.0
         self.flags = 0
         self.plane_fn = None          # optional: planes -> first plane (multi-GPU offsets)
+        self.names = fused_names(model) if tables is not None else None   # weight keys by role (Adam slots)
 
     def _tables(self):
         return self.tables if self.tables is not None else self.model._fused_tables()
@@ -312,7 +313,7 @@ class FusedStep:
     def apply_adam(self, optimizer):
         optimizer.iterations += 1
         t = self._tables()
-        names = fused_names(self.model)
+        names = self.names or fused_names(self.model)
         g = self.grad_buffers()
         slot = {"ent": 0, "rel": 1, "rel_aux": 2, "ent_aux": 3}
         for role, buf in zip(self.grad_roles(), g):

@@ -89,7 +89,7 @@ class Exchange:
 class ShardedStep:
     """Drop-in for ``FusedStep`` across G ranks (see module docstring)."""
 
-    def __init__(self, model, exchange=None, mode="auto"):
+    def __init__(self, model, exchange=None, mode="auto", local_fast=True):
         self.model = model
         self.ex = exchange or Exchange()
         G, g = self.ex.world, self.ex.rank
@@ -158,6 +158,15 @@ class ShardedStep:
             self.fused = f
         elif engine.backend() != "eager":
             raise RuntimeError("ShardedStep needs GPUs (or KGE_BACKEND=eager for host-only tests)")
+        # one rank: every row is local, so the fused single-device step runs on
+        # the shard itself (in-kernel SGD, compact update launch) -- no cache
+        self.direct = None
+        if self.fused is not None and G == 1 and mode == "sparse" and local_fast:
+            td = dict(t)
+            td["ent"] = self.shard[:, :self.ce].view(self.ent_shape)
+            if self.ca:
+                td["ent_aux"] = self.shard[:, self.ce:]
+            self.direct = engine.FusedStep(model, tables=td)
 
     def _ecols(self):
         return [self.ce] + ([self.ca] if self.ca else [])
@@ -216,26 +225,28 @@ class ShardedStep:
         return torch.stack([outs[0].view(B, Ks), outs[1].view(B, Ks)], dim=-1).reshape(-1)
 
     def _fetch_sparse(self, ids):
-        """Unique ids -> row cache in request order + the remap of ``ids``."""
-        G, g, ex = self.G, self.g, self.ex
-        uniq = torch.unique(ids)
-        own = uniq % G
-        order = torch.argsort(own, stable=True)
-        req = uniq[order]
+        """Unique ids -> row cache + the remap of ``ids`` to cache rows. One
+        sort: unique of the owner-major key (owner, id), so the cache order is
+        the request order and the inverse index is the remap."""
+        G, ex, E = self.G, self.ex, self.E
+        key = (ids % G) * E + ids if G > 1 else ids
+        uniq, inv = torch.unique(key, return_inverse=True)
+        U = int(uniq.shape[0])
+        cache = self._cache_buf(U)
+        if G == 1:   # every row is local: gather straight into the cache
+            torch.index_select(self.shard, 0, uniq, out=cache[:U])
+            return cache, inv, (None, None, uniq)
+        own = torch.div(uniq, E, rounding_mode="floor")
+        req = uniq - own * E
         send = torch.bincount(own, minlength=G)
         recv = torch.empty_like(send)
         ex.all_to_all(recv, send)
-        sc, rc = send.tolist(), recv.tolist()       # the one host sync of the step
+        sc, rc = send.tolist(), recv.tolist()
         rids = torch.empty(sum(rc), dtype=req.dtype, device=req.device)
         ex.all_to_all(rids, req, rc, sc)
-        rows = self.shard[torch.div(rids, G, rounding_mode="floor")]
-        U = int(req.shape[0])
-        cache = self._cache_buf(U)
+        rows = torch.index_select(self.shard, 0, torch.div(rids, G, rounding_mode="floor"))
         ex.all_to_all(cache[:U], rows, sc, rc)
-        inv = torch.empty_like(order)
-        inv[order] = torch.arange(U, device=order.device)
-        remap = inv[torch.searchsorted(uniq, ids)]
-        return cache, remap, (sc, rc, rids)
+        return cache, inv, (sc, rc, rids)
 
     def _cache_buf(self, U):
         """The row cache at a FIXED capacity (the kernel's table shape, hence
@@ -326,49 +337,57 @@ class ShardedStep:
         return 0 if k == 0 else 3
 
     def _apply_sparse(self, optimizer, gbufs, sc, rc, rids):
-        """Gradient rows back to their owners, owner-side sum + apply."""
+        """Gradient rows back to their owners; the owner applies each source
+        rank's rows in rank order (rows unique within a source: no write
+        conflicts, deterministic; duplicates across sources are added one
+        after the other, as keras SGD's scatter-add of IndexedSlices does)."""
         G, ex = self.G, self.ex
-        n_in = sum(rc)
-        U = sum(sc)            # this rank's unique rows = its cache rows [0, U)
-        lidx = torch.div(rids, G, rounding_mode="floor")
-        touched = torch.unique(lidx)
-        pos = torch.searchsorted(touched, lidx)
-        bounds = [0]
-        for c in rc:
-            bounds.append(bounds[-1] + c)
+        local = G == 1
+        U = rids.shape[0] if local else sum(sc)
+        lidx = rids if local else torch.div(rids, G, rounding_mode="floor")
+        bounds = [0, U] if local else [0]
+        if not local:
+            for c in rc:
+                bounds.append(bounds[-1] + c)
         adam = isinstance(optimizer, _opt.Adam)
         for k, gb in enumerate(gbufs):
             cols = gb.shape[1]
-            back = torch.empty(n_in, cols, dtype=torch.float32, device=gb.device)
-            ex.all_to_all(back, gb[:U].contiguous(), rc, sc)
-            # each source's rows are unique: index_add_ per source is collision-free
-            acc = torch.zeros(touched.shape[0] if not adam else self.Es, cols, dtype=torch.float32,
-                              device=gb.device)
-            tgt = pos if not adam else lidx
-            for s in range(G):
-                a, b = bounds[s], bounds[s + 1]
-                if b > a:
-                    acc.index_add_(0, tgt[a:b], back[a:b])
+            if local:
+                back = gb[:U]
+            else:
+                back = torch.empty(bounds[-1], cols, dtype=torch.float32, device=gb.device)
+                ex.all_to_all(back, gb[:U].contiguous(), rc, sc)
             lo = 0 if k == 0 else self.ce
             var = self.shard[:, lo:lo + cols]
             v = self._slot(k)
-            if adam:
+            if adam:   # keras Adam decays every row: a dense gradient of the shard
+                acc = torch.zeros(self.Es, cols, dtype=torch.float32, device=gb.device)
+                for s in range(len(bounds) - 1):
+                    if bounds[s + 1] > bounds[s]:
+                        acc.index_add_(0, lidx[bounds[s]:bounds[s + 1]], back[bounds[s]:bounds[s + 1]])
                 self._apply_dense(var[:self.valid], acc[:self.valid], v, optimizer, self._shard_name(k))
-            elif self.fused is not None:
-                a = _hip.kge_apply_rows_desc()
-                a.var = _hip.table(var)
-                a.rows = touched.data_ptr()
-                a.n = int(touched.shape[0])
-                a.grad = acc.data_ptr()
-                a.grad_ld = cols
-                a.norm2 = self.norm2.data_ptr() + 4 * v
-                a.lr = optimizer.learning_rate
-                a.clip_norm = 5.0
-                _hip.check(self.lib.kge_apply_rows(ctypes.byref(a), _hip.stream_handle(var.device)), "kge_apply_rows")
-            else:
-                with torch.no_grad():
-                    cs = 5.0 / max(math.sqrt(float(self.norm2[v])), 5.0)
-                    var[touched] = var[touched] + (acc * cs) * (-optimizer.learning_rate)
+                continue
+            for s in range(len(bounds) - 1):
+                a, b = bounds[s], bounds[s + 1]
+                if b == a:
+                    continue
+                if self.fused is not None:
+                    d = _hip.kge_apply_rows_desc()
+                    d.var = _hip.table(var)
+                    d.rows = lidx.data_ptr() + 8 * a
+                    d.n = b - a
+                    d.grad = back.data_ptr() + 4 * a * back.stride(0)
+                    d.grad_ld = back.stride(0)
+                    d.norm2 = self.norm2.data_ptr() + 4 * v
+                    d.lr = optimizer.learning_rate
+                    d.clip_norm = 5.0
+                    _hip.check(self.lib.kge_apply_rows(ctypes.byref(d), _hip.stream_handle(var.device)),
+                               "kge_apply_rows")
+                else:
+                    with torch.no_grad():
+                        cs = 5.0 / max(math.sqrt(float(self.norm2[v])), 5.0)
+                        li = lidx[a:b]
+                        var[li] = var[li] + (back[a:b] * cs) * (-optimizer.learning_rate)
 
     def _shard_name(self, k):
         return self.names["ent" if k == 0 else "ent_aux"] + "#shard"
@@ -389,6 +408,8 @@ class ShardedStep:
 
     # ------------------------------------------------------------ step
     def __call__(self, batch, is_train, optimizer, neg_ids=None, prof_events=None):
+        if self.direct is not None:
+            return self.direct(batch, is_train, optimizer, neg_ids=neg_ids, prof_events=prof_events)
         if isinstance(optimizer, _opt.Adam) and is_train:
             optimizer.iterations += 1
         self._constrain()
@@ -471,6 +492,8 @@ class ShardedStep:
         self.sync()
 
     def check_status(self):
+        if self.direct is not None:
+            self.direct.check_status()
         if self.fused is not None:
             _hip.check_device_status(self.status, "kge_step")
 

@@ -589,7 +589,7 @@ def test_fused_adam_first_step(hiplib, model_name):
     check(ref, got, l_, ps, ns)
 
 
-@pytest.mark.parametrize("mode", ["sparse", "dense"])
+@pytest.mark.parametrize("mode", ["sparse", "dense", "local"])
 @pytest.mark.parametrize("model_name,score_kind", [("TransE", "lp2"), ("TransD", "lppow2"), ("RotatE", "lp1"),
                                                    ("TransR", "lppow2"), ("DistMult", None)])
 def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
@@ -620,7 +620,10 @@ def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
         m = _make(model_name, d, K, "h+t", sc, loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E, R,
                   UniformStrategy(np.arange(E), seed=9), k=k)
         m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
-        st = ShardedStep(m, mode=mode)
+        # "sparse" forces the exchange + row cache even on one rank; "local" is
+        # the one-rank shortcut (the fused step directly on the shard)
+        st = ShardedStep(m, mode="sparse" if mode == "local" else mode, local_fast=mode == "local")
+        assert (st.direct is not None) == (mode == "local")
         ref_w = W
         opt = optimizers.SGD(0.05)
         for it in range(2):
@@ -673,7 +676,7 @@ def test_sharded_step_c5_shard_size(hiplib):
             m = _make("TransE", d, K, "h+t", score.LpDistance(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
                       E, R, UniformStrategy(np.arange(E), seed=5), constraint=False)
             m.model_weights = {"ent_emb": ent.clone(), "rel_emb": rel.clone()}
-            stp = ShardedStep(m, mode="sparse") if sharded else engine.FusedStep(m)
+            stp = ShardedStep(m, mode="sparse", local_fast=False) if sharded else engine.FusedStep(m)
             lv = float(stp(pos, True, optimizers.SGD(0.01)))
             torch.cuda.synchronize()
             stp.check_status()
