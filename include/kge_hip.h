@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KGE_ABI_VERSION 2
+#define KGE_ABI_VERSION 3
 
 typedef enum kge_status {
   KGE_OK = 0,
@@ -214,6 +214,14 @@ typedef struct kge_step_desc {
   int32_t _pad;
   float* grad_out[4];         /* KGE_OPT_GRAD: dense [rows, cols] gradient per
                                  variable (order as norm2_out; row stride cols) */
+  /* multi-GPU (KGE/sharded.py): ent / ent_aux hold shard_count all-gathered
+   * shards of shard_rows rows each, entity id e at row
+   * (e mod shard_count) * shard_rows + e div shard_count; ids (triples and
+   * draws) stay global, in [0, global_entities). shard_count <= 1: identity. */
+  int64_t shard_rows;
+  int64_t global_entities;
+  int32_t shard_count;
+  int32_t _pad3;
 } kge_step_desc;
 
 /*

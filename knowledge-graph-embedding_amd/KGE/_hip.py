@@ -11,7 +11,7 @@ import threading
 
 import torch
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 KGE_OK, KGE_EINVAL, KGE_ERANGE, KGE_EHIP, KGE_ENOMEM_WORKSPACE, KGE_EUNSUPPORTED = range(6)
 
@@ -68,6 +68,8 @@ class kge_step_desc(ctypes.Structure):
         ("prof_events", ctypes.c_void_p),
         ("flags", ctypes.c_int32), ("_pad", ctypes.c_int32),
         ("grad_out", ctypes.c_void_p * 4),
+        ("shard_rows", ctypes.c_int64), ("global_entities", ctypes.c_int64),
+        ("shard_count", ctypes.c_int32), ("_pad3", ctypes.c_int32),
     ]
 
 

@@ -149,6 +149,7 @@ class FusedStep:
         self.batch_scale = 1.0
         self.flags = 0
         self.plane_fn = None          # optional: planes -> first plane (multi-GPU offsets)
+        self.shard = None             # optional (G, shard_rows, global E): the tables are gathered shards
         self.names = fused_names(model) if tables is not None else None   # weight keys by role (Adam slots)
 
     def _tables(self):
@@ -225,6 +226,8 @@ class FusedStep:
             d.lr = optimizer.learning_rate
         d.clip_norm = 5.0
         d.flags = self.flags
+        if self.shard is not None:
+            d.shard_count, d.shard_rows, d.global_entities = self.shard
         if d.optimizer == _hip.OPT_GRAD:
             g = self.grad_buffers()
             slot = {"ent": 0, "rel": 1, "rel_aux": 2, "ent_aux": 3}

@@ -91,7 +91,7 @@ def fused_descriptor(score_fn):
     if type(score_fn) in (LpDistance, LpDistancePow):
         p = score_fn.p
         p = float("inf") if p == math.inf else float(p)
-        if p not in (1.0, 2.0, float("inf")):
+        if not p > 0:       # p <= 0 / NaN: the plugin path (TF's own behaviour)
             return None
         return score_fn.kind, p
     if type(score_fn) is Dot:

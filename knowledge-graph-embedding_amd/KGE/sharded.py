@@ -155,6 +155,9 @@ class ShardedStep:
             f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT
             if mode == "sparse":   # every cache row [0, U) is a batch id: no gradient zero-fill
                 f.flags |= _hip.FLAG_GRAD_ROWS_TOUCHED
+            else:   # the kernels map global ids to rows of the gathered shards and draw in-register
+                f.shard = (G, self.Es, E)
+                f.plane_fn = lambda ns, n: ns.take_planes(n) * G + g * n
             self.fused = f
         elif engine.backend() != "eager":
             raise RuntimeError("ShardedStep needs GPUs (or KGE_BACKEND=eager for host-only tests)")
@@ -413,6 +416,15 @@ class ShardedStep:
         if isinstance(optimizer, _opt.Adam) and is_train:
             optimizer.iterations += 1
         self._constrain()
+        if self.mode == "dense" and self.fused is not None:
+            # global ids straight into kge_step: the kernels draw the negatives
+            # and map every id to its row of the gathered table
+            self.ex.all_gather(self.full, self.shard)
+            self._local_grads(batch, neg_ids, is_train, optimizer, self.full, self.gfull, prof_events)
+            self.ex.all_reduce(self.red)
+            if is_train:
+                self._dense_apply(optimizer)
+            return self.loss
         if neg_ids is None:
             neg_ids = self._draw(batch)
         Bn = int(batch.shape[0])
@@ -437,13 +449,18 @@ class ShardedStep:
             if self.mode == "sparse":
                 self._apply_sparse(optimizer, gbufs, *plan)
             else:
-                for k in range(len(gbufs)):
-                    self.ex.reduce_scatter(self.gshard[k], self.gfull[k])
-                    lo = 0 if k == 0 else self.ce
-                    var = self.shard[:self.valid, lo:lo + gbufs[k].shape[1]]
-                    self._apply_dense(var, self.gshard[k][:self.valid], self._slot(k), optimizer, self._shard_name(k))
+                self._dense_apply(optimizer, apply_rel=False)
             self._apply_rel(optimizer)
         return self.loss
+
+    def _dense_apply(self, optimizer, apply_rel=True):
+        for k in range(len(self.gfull)):
+            self.ex.reduce_scatter(self.gshard[k], self.gfull[k])
+            lo = 0 if k == 0 else self.ce
+            var = self.shard[:self.valid, lo:lo + self.gfull[k].shape[1]]
+            self._apply_dense(var, self.gshard[k][:self.valid], self._slot(k), optimizer, self._shard_name(k))
+        if apply_rel:
+            self._apply_rel(optimizer)
 
     # ------------------------------------------------------------ state
     def release_entity_tables(self):

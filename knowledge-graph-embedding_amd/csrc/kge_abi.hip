@@ -56,7 +56,7 @@ struct Plan {
 int score_sk(int kind, float p) {
   if (kind == KGE_SCORE_DOT) return SK_DOT;
   if (std::isinf(p)) return SK_PINF;
-  return p == 1.f ? SK_P1 : SK_P2;
+  return p == 1.f ? SK_P1 : p == 2.f ? SK_P2 : SK_PGEN;
 }
 
 kge_status check_table(const kge_table& t, const char* name, int64_t cols) {
@@ -109,6 +109,14 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     if (d->dim > kTrMaxDim || d->dim_rel > kTrMaxDim)
       return fail(KGE_EUNSUPPORTED, "TransR fused step supports embedding sizes <= %d", kTrMaxDim);
   }
+  if (d->shard_count > 1) {
+    if (rescal || (model == KGE_MODEL_TRANSH && d->constraint))
+      return fail(KGE_EUNSUPPORTED, "sharded tables: full-table regulariser models are not sharded");
+    if (d->shard_rows <= 0 || d->global_entities <= 0 ||
+        d->global_entities > (int64_t)d->shard_count * d->shard_rows ||
+        d->ent.rows < (int64_t)d->shard_count * d->shard_rows)
+      return fail(KGE_EINVAL, "sharded tables: need shard_count * shard_rows >= global_entities rows");
+  }
   if (d->batch < 0) return fail(KGE_EINVAL, "batch must be >= 0");
   if (d->negative_ratio < 0) return fail(KGE_EINVAL, "negative_ratio must be >= 0");
   if (d->corrupt_side < KGE_SIDE_H || d->corrupt_side > KGE_SIDE_HT)
@@ -121,8 +129,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   if (d->score_kind < KGE_SCORE_LP || d->score_kind > KGE_SCORE_DOT)
     return fail(KGE_EINVAL, "unknown score kind %d", d->score_kind);
   const float p = d->score_p;
-  if (d->score_kind != KGE_SCORE_DOT && !(p == 1.f || p == 2.f || std::isinf(p)))
-    return fail(KGE_EUNSUPPORTED, "fused Lp score supports p in {1, 2, inf} (got %g)", (double)p);
+  if (d->score_kind != KGE_SCORE_DOT && !(p > 0.f))
+    return fail(KGE_EINVAL, "Lp score needs p > 0 (got %g)", (double)p);
   if (model == KGE_MODEL_ROTATE && d->score_kind == KGE_SCORE_DOT)
     return fail(KGE_EUNSUPPORTED, "RotatE with Dot() yields a complex score");
   if (model == KGE_MODEL_ROTATE && !(d->rotate_limit > 0.f))
@@ -253,6 +261,9 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.sk = score_sk(d->score_kind, p);
 
   A.ent = TabView{d->ent.data, d->ent.ld, (int32_t)entc, E};
+  A.n_ent = d->shard_count > 1 ? d->global_entities : E;
+  A.rG = d->shard_count > 1 ? d->shard_count : 1;
+  A.rEs = d->shard_count > 1 ? d->shard_rows : 0;
   A.rel = TabView{d->rel.data, d->rel.ld, (int32_t)relc, R};
   A.pos = d->pos;
   A.i64 = d->idx_dtype == KGE_IDX_I64;
@@ -284,6 +295,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.inv_b = (float)(1.0 / bg);
   A.inv_bk = (float)(1.0 / (bg * Keff));
   A.limit = d->rotate_limit;
+  A.p = d->score_p;
   A.rel_reg = (model == KGE_MODEL_DISTMULT && d->constraint) ? d->constraint_weight : 0.f;
   A.rel_dests = !rescal;
   A.dense = rescal && A.train;
@@ -699,8 +711,8 @@ kge_status kge_rank(const kge_rank_desc* d, void* stream) {
   if ((d->filt_beg == nullptr) != (d->filt_end == nullptr) || (d->filt_beg && !d->filt_ent))
     return fail(KGE_EINVAL, "filter needs filt_beg, filt_end and filt_ent");
   const float p = d->score_p;
-  if (d->score_kind != KGE_SCORE_DOT && !(p == 1.f || p == 2.f || std::isinf(p)))
-    return fail(KGE_EUNSUPPORTED, "ranking Lp score supports p in {1, 2, inf} (got %g)", (double)p);
+  if (d->score_kind != KGE_SCORE_DOT && !(p > 0.f))
+    return fail(KGE_EINVAL, "Lp score needs p > 0 (got %g)", (double)p);
   if (3 * kRankQ * ((d->dim + 3) & ~3) * 4 > 64 * 1024) return fail(KGE_EUNSUPPORTED, "query rows too wide");
   RankArgs A{};
   A.cand = d->cand.data;
@@ -714,6 +726,7 @@ kge_status kge_rank(const kge_rank_desc* d, void* stream) {
   A.clip = d->clip != 0;
   A.hside = hside;
   A.pw = d->score_kind == KGE_SCORE_LP_POW;
+  A.p = p;
   A.q0 = d->q0;
   A.q1 = d->q1;
   A.qw = d->qw;

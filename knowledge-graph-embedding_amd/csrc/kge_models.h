@@ -16,7 +16,9 @@
 namespace kge {
 
 enum { KIND_POS = 0, KIND_HC = 1, KIND_TC = 2 };
-enum { SK_P1 = 0, SK_P2 = 1, SK_PINF = 2, SK_DOT = 3 };
+enum { SK_P1 = 0, SK_P2 = 1, SK_PINF = 2, SK_DOT = 3, SK_PGEN = 4 };
+// SK_PGEN: LpDistance(p) for any finite p > 0 (score.py:49-63); its runtime p
+// travels in the `M` argument the p = inf kind uses for the row maximum
 
 constexpr float kPiF = 3.14159265358979323846f;
 
@@ -32,7 +34,7 @@ __device__ __forceinline__ float cmod(float re, float im) {
 // a = x - y (Lp kinds) or a = x, b = y (Dot). CPLX: (re, im) interleaved and
 // |.| is the complex modulus (score.py:59-63 on complex64 input).
 template <int SK, bool CPLX, int VEC, int NC>
-__device__ __forceinline__ float score_partial(const Frag<VEC, NC>& a, const Frag<VEC, NC>& b) {
+__device__ __forceinline__ float score_partial(const Frag<VEC, NC>& a, const Frag<VEC, NC>& b, float p = 2.f) {
   float acc = 0.f;
   if (SK == SK_DOT) {
 #pragma unroll
@@ -44,6 +46,7 @@ __device__ __forceinline__ float score_partial(const Frag<VEC, NC>& a, const Fra
     for (int i = 0; i < VEC * NC; i += 2) {
       if (SK == SK_P2) acc += a.v[i] * a.v[i] + a.v[i + 1] * a.v[i + 1];
       else if (SK == SK_P1) acc += cmod(a.v[i], a.v[i + 1]);
+      else if (SK == SK_PGEN) acc += powf(cmod(a.v[i], a.v[i + 1]), p);
       else acc = fmaxf(acc, cmod(a.v[i], a.v[i + 1]));
     }
   } else {
@@ -52,6 +55,7 @@ __device__ __forceinline__ float score_partial(const Frag<VEC, NC>& a, const Fra
       const float m = fabsf(a.v[i]);
       if (SK == SK_P2) acc += m * m;
       else if (SK == SK_P1) acc += m;
+      else if (SK == SK_PGEN) acc += powf(m, p);
       else acc = fmaxf(acc, m);
     }
   }
@@ -78,11 +82,12 @@ __device__ __forceinline__ float tie_partial(const Frag<VEC, NC>& a, float M) {
 //   LpDistancePow: -(LpDistance)^2
 //   Dot:           R
 template <int SK>
-__device__ __forceinline__ float score_value(float R, bool pw, float* lp_out) {
+__device__ __forceinline__ float score_value(float R, bool pw, float* lp_out, float p = 2.f) {
   if (SK == SK_DOT) { *lp_out = R; return R; }
   float lp;
   if (SK == SK_P2) lp = -sqrtf(fmaxf(R, 1e-9f));
   else if (SK == SK_P1) lp = -fmaxf(R, 1e-9f);
+  else if (SK == SK_PGEN) lp = -powf(fmaxf(R, 1e-9f), 1.f / p);
   else lp = -R;
   *lp_out = lp;
   return pw ? -(lp * lp) : lp;
@@ -92,13 +97,16 @@ __device__ __forceinline__ float score_value(float R, bool pw, float* lp_out) {
 //   P2:   g_a = alpha * a                       (TF: pow/clip/sum/pow/abs chain)
 //   P1:   g_a = alpha * sign(a) (complex: a/|a|)
 //   PINF: g_a = alpha * sign(a) on the arg-max set (ties split evenly)
+//   PGEN: g_a = alpha * |a|^(p-1) sign(a) (complex: |a|^(p-2) a),
+//         alpha = -c R^(1/p - 1)   (d/dR of -R^(1/p) times d|a|^p/da / p)
 //   DOT:  g_x = alpha * y, g_y = alpha * x
 template <int SK>
-__device__ __forceinline__ float score_alpha(float c, float R, float lp, float ties, bool pw) {
+__device__ __forceinline__ float score_alpha(float c, float R, float lp, float ties, bool pw, float p = 2.f) {
   if (SK == SK_DOT) return c;
   const float clp = pw ? c * (-2.f * lp) : c;   // d(-lp^2)/dlp = -2 lp
   if (SK == SK_P2) return R >= 1e-9f ? (-clp * 0.5f * rsqrtf(R)) * 2.f : 0.f;
   if (SK == SK_P1) return R >= 1e-9f ? -clp : 0.f;
+  if (SK == SK_PGEN) return R >= 1e-9f ? -clp * powf(R, 1.f / p - 1.f) : 0.f;
   return -clp / ties;
 }
 
@@ -106,7 +114,8 @@ __device__ __forceinline__ float score_alpha(float c, float R, float lp, float t
 // for the score kernel's in-stream weights; the stored per-negative
 // coefficients and scores use the IEEE forms above.
 template <int SK>
-__device__ __forceinline__ float score_value_fast(float R, bool pw, float* lp_out) {
+__device__ __forceinline__ float score_value_fast(float R, bool pw, float* lp_out, float p = 2.f) {
+  if (SK == SK_PGEN) return score_value<SK>(R, pw, lp_out, p);
   if (SK == SK_DOT) { *lp_out = R; return R; }
   float lp;
   if (SK == SK_P2) lp = -__builtin_amdgcn_sqrtf(fmaxf(R, 1e-9f));
@@ -116,7 +125,8 @@ __device__ __forceinline__ float score_value_fast(float R, bool pw, float* lp_ou
   return pw ? -(lp * lp) : lp;
 }
 template <int SK>
-__device__ __forceinline__ float score_alpha_fast(float c, float R, float lp, float ties, bool pw) {
+__device__ __forceinline__ float score_alpha_fast(float c, float R, float lp, float ties, bool pw, float p = 2.f) {
+  if (SK == SK_PGEN) return score_alpha<SK>(c, R, lp, ties, pw, p);
   if (SK == SK_DOT) return c;
   const float clp = pw ? c * (-2.f * lp) : c;
   if (SK == SK_P2) return R >= 1e-9f ? -clp * __builtin_amdgcn_rsqf(R) : 0.f;
@@ -133,6 +143,22 @@ __device__ __forceinline__ void score_grad(const Frag<VEC, NC>& a, float alpha, 
   if (SK == SK_P2) {
 #pragma unroll
     for (int i = 0; i < VEC * NC; ++i) g.v[i] = alpha * a.v[i];
+    return;
+  }
+  if (SK == SK_PGEN) {   // M carries p
+#pragma unroll
+    for (int i = 0; i < VEC * NC; i += (CPLX ? 2 : 1)) {
+      if (CPLX) {
+        const float m = cmod(a.v[i], a.v[i + 1]);
+        const float s = m > 0.f ? alpha * powf(m, M - 2.f) : 0.f;
+        g.v[i] = s * a.v[i];
+        g.v[i + 1] = s * a.v[i + 1];
+      } else {
+        const float x = a.v[i];
+        const float s = x > 0.f ? alpha : (x < 0.f ? -alpha : 0.f);
+        g.v[i] = x != 0.f ? s * powf(fabsf(x), M - 1.f) : 0.f;
+      }
+    }
     return;
   }
   if (CPLX) {

@@ -227,12 +227,12 @@ __device__ __forceinline__ void score_xy_grad(const Frag<VEC, NC>& x, const Frag
 }
 
 template <int SK, int VEC, int NC>
-__device__ __forceinline__ float score_xy_partial(const Frag<VEC, NC>& x, const Frag<VEC, NC>& y) {
+__device__ __forceinline__ float score_xy_partial(const Frag<VEC, NC>& x, const Frag<VEC, NC>& y, float p) {
   if (SK == SK_DOT) return dot_partial(x, y);
   Frag<VEC, NC> a;
 #pragma unroll
   for (int i = 0; i < VEC * NC; ++i) a.v[i] = x.v[i] - y.v[i];
-  return score_partial<SK, false>(a, a);
+  return score_partial<SK, false>(a, a, p);
 }
 
 template <int VEC, int NC>
@@ -266,9 +266,9 @@ __global__ __launch_bounds__(kPjThreads) void proj_kernel(StepArgs A, PjArgs P) 
   int64_t ph = load_idx(A.pos, i * 3 + 0, A.i64);
   int64_t pr = load_idx(A.pos, i * 3 + 1, A.i64);
   int64_t pt = load_idx(A.pos, i * 3 + 2, A.i64);
-  if (ph < 0 || ph >= A.ent.rows) { err = KGE_ERANGE; ph = 0; }
+  ph = ent_row(A, ph, &err);
   if (pr < 0 || pr >= A.rel.rows) { err = KGE_ERANGE; pr = 0; }
-  if (pt < 0 || pt >= A.ent.rows) { err = KGE_ERANGE; pt = 0; }
+  pt = ent_row(A, pt, &err);
   for (int j = tid; j < K; j += kPjThreads) ids[j] = slot_entity(A, i, j, &err);
 
   // ---- the positive's rows and projections (every wave keeps its own copy)
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(kPjThreads) void proj_kernel(StepArgs A, PjArgs P) 
         x[u].v[q] = hc ? Pr[u].v[q] + Rv.v[q] : X.v[q];
         y[u].v[q] = hc ? PT.v[q] : Pr[u].v[q];
       }
-      part[u] = score_xy_partial<SK>(x[u], y[u]);
+      part[u] = score_xy_partial<SK>(x[u], y[u], A.p);
     }
     wave_sums<U, SK == SK_PINF>(part);
     float tq[U];
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(kPjThreads) void proj_kernel(StepArgs A, PjArgs P) 
           float lp;
           sR[q0 + u] = part[u];
           sT[q0 + u] = tq[u];
-          sS[q0 + u] = score_value<SK>(part[u], A.pw, &lp);
+          sS[q0 + u] = score_value<SK>(part[u], A.pw, &lp, A.p);
           sD[q0 + u] = dt[u];
           sN[q0 + u] = nr[u];
         }
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(kPjThreads) void proj_kernel(StepArgs A, PjArgs P) 
   }
   // the positive's score (wave 0)
   if (wv == 0) {
-    float part[1] = {score_xy_partial<SK>(X, PT)};
+    float part[1] = {score_xy_partial<SK>(X, PT, A.p)};
     wave_sums<1, SK == SK_PINF>(part);
     float tq = 1.f;
     if (SK == SK_PINF) {
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(kPjThreads) void proj_kernel(StepArgs A, PjArgs P) 
       float lp;
       sR[K] = part[0];
       sT[K] = tq;
-      sS[K] = score_value<SK>(part[0], A.pw, &lp);
+      sS[K] = score_value<SK>(part[0], A.pw, &lp, A.p);
     }
   }
   __syncthreads();
@@ -391,9 +391,9 @@ __global__ __launch_bounds__(kPjThreads) void proj_kernel(StepArgs A, PjArgs P) 
     for (int q = lane; q < K; q += KGE_WAVE) {
       const float s = sS[q];
       float lp;
-      score_value<SK>(sR[q], A.pw, &lp);
+      score_value<SK>(sR[q], A.pw, &lp, A.p);
       const float c = neg_coef(A, s, sp, Ms, invZ);
-      sA[q] = score_alpha<SK>(c, sR[q], lp, sT[q], A.pw);
+      sA[q] = score_alpha<SK>(c, sR[q], lp, sT[q], A.pw, A.p);
       csum += c;
       switch (A.loss_kind) {
         case KGE_LOSS_HINGE: lneg += fmaxf(A.margin + s - sp, 0.f); break;
@@ -418,8 +418,8 @@ __global__ __launch_bounds__(kPjThreads) void proj_kernel(StepArgs A, PjArgs P) 
         default: lossp = ((sp - 1.f) * (sp - 1.f) + lneg) * 0.5f * A.inv_b; cp = (sp - 1.f) * A.inv_b; break;
       }
       float lpp;
-      score_value<SK>(sR[K], A.pw, &lpp);
-      sA[K] = score_alpha<SK>(cp, sR[K], lpp, sT[K], A.pw);
+      score_value<SK>(sR[K], A.pw, &lpp, A.p);
+      sA[K] = score_alpha<SK>(cp, sR[K], lpp, sT[K], A.pw, A.p);
       misc[0] = lossp;
       if (A.pos_score_out) A.pos_score_out[i] = sp;
     }
@@ -465,7 +465,7 @@ __global__ __launch_bounds__(kPjThreads) void proj_kernel(StepArgs A, PjArgs P) 
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const float alpha = q0 + u < K ? sA[qq[u]] : 0.f;   // rows past the range: weight 0
-        const float M = sR[qq[u]];
+        const float M = SK == SK_PGEN ? A.p : sR[qq[u]];
         F x, y;
 #pragma unroll
         for (int q = 0; q < VEC * NC; ++q) {
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(kPjThreads) void proj_kernel(StepArgs A, PjArgs P) 
     // the positive's own triple (wave 0)
     if (wv == 0) {
       F g[2], gW[2], gE[2], gQ[2];
-      score_xy_grad<SK>(X, PT, sA[K], sR[K], g[0], g[1]);
+      score_xy_grad<SK>(X, PT, sA[K], SK == SK_PGEN ? A.p : sR[K], g[0], g[1]);
       add_to(accR, g[0]);
       nrm[1] += sq_partial(g[0]);
       const F* er[2] = {&H, &T};

@@ -16,6 +16,7 @@ static void pj_sk(const StepArgs& A, const PjArgs& P, int sk, hipStream_t st) {
     case SK_P1: pj_launch<VEC, NC, SK_P1>(A, P, st); break;
     case SK_P2: pj_launch<VEC, NC, SK_P2>(A, P, st); break;
     case SK_PINF: pj_launch<VEC, NC, SK_PINF>(A, P, st); break;
+    case SK_PGEN: pj_launch<VEC, NC, SK_PGEN>(A, P, st); break;
     default: pj_launch<VEC, NC, SK_DOT>(A, P, st); break;
   }
 }

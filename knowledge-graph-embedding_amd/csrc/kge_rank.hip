@@ -50,6 +50,7 @@ __device__ __forceinline__ void rank_scores(const RankArgs& A, int64_t e, const 
     const float m = fabsf(a);
     if (SK == SK_P2) ac = ac + m * m;
     else if (SK == SK_P1) ac = ac + m;
+    else if (SK == SK_PGEN) ac = ac + powf(m, A.p);
     else ac = fmaxf(ac, m);
   };
   if (MODE == KGE_RANK_ROT) {
@@ -73,7 +74,7 @@ __device__ __forceinline__ void rank_scores(const RankArgs& A, int64_t e, const 
         if (SK == SK_P2) acc[j] = acc[j] + (ar * ar + ai * ai);
         else {
           const float m = sqrtf(ar * ar + ai * ai);
-          acc[j] = SK == SK_P1 ? acc[j] + m : fmaxf(acc[j], m);
+          acc[j] = SK == SK_P1 ? acc[j] + m : SK == SK_PGEN ? acc[j] + powf(m, A.p) : fmaxf(acc[j], m);
         }
       }
     }
@@ -145,7 +146,7 @@ __device__ __forceinline__ void rank_scores(const RankArgs& A, int64_t e, const 
       out[j] = acc[j];
     } else {
       float lpv;
-      out[j] = score_value<SK>(acc[j], A.pw, &lpv);
+      out[j] = score_value<SK>(acc[j], A.pw, &lpv, A.p);
     }
   }
 }
@@ -238,6 +239,7 @@ static void rank_by_sk(const RankArgs& A, int sk, hipStream_t st) {
     case SK_P1: rank_launch<MODE, PJ, SK_P1>(A, st); break;
     case SK_P2: rank_launch<MODE, PJ, SK_P2>(A, st); break;
     case SK_PINF: rank_launch<MODE, PJ, SK_PINF>(A, st); break;
+    case SK_PGEN: rank_launch<MODE, PJ, SK_PGEN>(A, st); break;
     default: rank_launch<MODE, PJ, SK_DOT>(A, st); break;
   }
 }

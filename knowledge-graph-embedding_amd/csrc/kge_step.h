@@ -53,6 +53,7 @@ struct StepArgs {
   float inv_b;      // 1 / (B * batch_scale)
   float inv_bk;     // 1 / (B * Keff * batch_scale)
   float limit;
+  float p;          // LpDistance p (SK_PGEN)
   float rel_reg;    // DistMult constraint_weight (0 = off): lambda * mean_i ||r_i||^2
   float lr, clip_norm;
   // dense-gradient variables (a full-table regulariser term makes TF's
@@ -77,6 +78,11 @@ struct StepArgs {
   // main pass; scale[] slots of the pass's entity / relation variable
   bool keep_cnt = false;
   bool rel_only = false;   // visit the relation destinations only (TransH rel_hyper pass)
+  // entity ids -> table rows: n_ent global ids; rG > 1: the table is G
+  // all-gathered shards of rEs rows, id e at (e mod rG) * rEs + e div rG
+  int64_t n_ent = 0;
+  int32_t rG = 1;
+  int64_t rEs = 0;
   int32_t sc_ent_idx = 0, sc_rel_idx = 1;
   // geometry
   int32_t wpp;      // waves per positive (1, 2, 4, 8)
@@ -223,6 +229,7 @@ struct RankArgs {
   bool clip;                              // TransD: projected rows clipped to norm <= 1
   bool hside;                             // corrupt_side 'h'
   bool pw;                                // LpDistancePow
+  float p;                                // LpDistance p (SK_PGEN)
   const float* q0; const float* q1; const float* qw; int64_t ldq;
   const void* true_ids; bool i64; int64_t n;
   const int64_t* fbeg; const int64_t* fend; const void* fent;

@@ -130,6 +130,14 @@ __device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_
   }
 }
 
+// global entity id -> its row of the step's entity table, range-checked:
+// the identity, or (multi-GPU, KGE/sharded.py) the row of id e in the
+// all-gathered shards, (e mod G) * shard_rows + e div G
+__device__ __forceinline__ int64_t ent_row(const StepArgs& A, int64_t e, int* err) {
+  if (e < 0 || e >= A.n_ent) { *err = KGE_ERANGE; return 0; }
+  return A.rG > 1 ? (e % A.rG) * A.rEs + e / A.rG : e;
+}
+
 // slot j of positive i: its entity id (drawn, or read from the caller's
 // negatives), bounds-checked; a drawn id is handed back when asked
 __device__ __forceinline__ int32_t slot_entity(const StepArgs& A, int64_t i, int j, int* err) {
@@ -140,15 +148,14 @@ __device__ __forceinline__ int32_t slot_entity(const StepArgs& A, int64_t i, int
     e = load_idx(A.neg_user, i * A.Keff + j, A.i64);
   } else {
     const int64_t x = load_idx(A.pos, i * 3 + (kind == KIND_HC ? 0 : 2), A.i64);
-    if (A.smp.kind == KGE_SAMPLER_TYPED && (x < 0 || x >= A.ent.rows)) { e = 0; *err = KGE_ERANGE; }
+    if (A.smp.kind == KGE_SAMPLER_TYPED && (x < 0 || x >= A.n_ent)) { e = 0; *err = KGE_ERANGE; }
     else {
       e = sample_entity(A.smp, A.smp.offset + poff, n, x, err);   // plane offset (+1 for the t side)
       if (e < 0) e = 0;
     }
     if (A.neg_user) store_idx(A.neg_user, i * A.Keff + j, e, A.i64);
   }
-  if (e < 0 || e >= A.ent.rows) { *err = KGE_ERANGE; e = 0; }
-  return (int32_t)e;
+  return (int32_t)ent_row(A, e, err);
 }
 
 // compile-time loop over u = 0 .. N-1 (fn gets std::integral_constant<int, u>)
@@ -233,9 +240,9 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
     ph = load_idx(A.pos, i * 3 + 0, A.i64);
     pr = load_idx(A.pos, i * 3 + 1, A.i64);
     pt = load_idx(A.pos, i * 3 + 2, A.i64);
-    if (ph < 0 || ph >= A.ent.rows) { err = KGE_ERANGE; ph = 0; }
+    ph = ent_row(A, ph, &err);
     if (pr < 0 || pr >= A.rel.rows) { err = KGE_ERANGE; pr = 0; }
-    if (pt < 0 || pt >= A.ent.rows) { err = KGE_ERANGE; pt = 0; }
+    pt = ent_row(A, pt, &err);
     if (gw == 0 && lane < 3) s_pos[grp * 3 + lane] = lane == 0 ? ph : lane == 1 ? pr : pt;
     for (int j = jbeg + lane; j < jend; j += KGE_WAVE) ids[j] = slot_entity(A, i, j, &err);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -256,10 +263,10 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
       F a, b, E0;
       E0.zero();
       M::fwd(ctx, KIND_POS, E0, a, b);
-      const float part = score_partial<SK, M::CPLX>(a, b);
+      const float part = score_partial<SK, M::CPLX>(a, b, A.p);
       Rp = lane_reduce<5, SK == SK_PINF>(part);
       if (SK == SK_PINF) tp = lane_reduce<5, false>(tie_partial<M::CPLX>(a, Rp));
-      sp = score_value<SK>(Rp, A.pw, &lpp);
+      sp = score_value<SK>(Rp, A.pw, &lpp, A.p);
     }
     const int lrow = lane >> SH;
     const bool lead = (lane & (LPR - 1)) == 0;
@@ -299,7 +306,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
       static_for<ROWS>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
         M::template fwdk<kind_at<SIDE>(u)>(ctx, E[u], a[u], b[u]);
-        part[u] = (u < nrow && (!RAW || lane_in)) ? score_partial<SK, M::CPLX>(a[u], b[u]) : 0.f;
+        part[u] = (u < nrow && (!RAW || lane_in)) ? score_partial<SK, M::CPLX>(a[u], b[u], A.p) : 0.f;
       });
       const float Rl = multi_reduce<ROWS, SK == SK_PINF>(part);
       float tl = 1.f;
@@ -314,7 +321,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
       // this lane's row weight dL/ds (loss.py; the loss VALUE is summed in
       // the finalise pass), hardware-rate transcendentals
       float lp;
-      const float s = score_value_fast<SK>(Rl, A.pw, &lp);
+      const float s = score_value_fast<SK>(Rl, A.pw, &lp, A.p);
       float c = 0.f;
       switch (A.loss_kind) {
         case KGE_LOSS_HINGE:
@@ -350,7 +357,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
           c = s * A.inv_b;
           break;
       }
-      const float al = valid ? score_alpha_fast<SK>(c, Rl, lp, tl, A.pw) : 0.f;
+      const float al = valid ? score_alpha_fast<SK>(c, Rl, lp, tl, A.pw, A.p) : 0.f;
       if (valid && lead) {
         gR[j] = Rl;
         gT[j] = tl;
@@ -364,7 +371,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
       static_for<ROWS>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
         const float alu = bcast(al, u << SH);
-        const float Mu = SK == SK_PINF ? bcast(Rl, u << SH) : 0.f;
+        const float Mu = SK == SK_PINF ? bcast(Rl, u << SH) : SK == SK_PGEN ? A.p : 0.f;
         M::template bwdk<kind_at<SIDE>(u)>(ctx, E[u], a[u], b[u], alu, Mu, accH, accR, accT, nrm, mp);
       });
     }
@@ -403,7 +410,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
       F pH, pR, pT, a, b, E0;
       pH.zero(); pR.zero(); pT.zero(); E0.zero();
       M::fwd(ctx, KIND_POS, E0, a, b);
-      M::bwd(ctx, KIND_POS, E0, a, b, 1.f, Rp, pH, pR, pT, pn, mp);
+      M::bwd(ctx, KIND_POS, E0, a, b, 1.f, SK == SK_PGEN ? A.p : Rp, pH, pR, pT, pn, mp);
       float* pg = posg + grp * 3 * FL;
 #pragma unroll
       for (int q = 0; q < VEC * NC; ++q) {
@@ -473,7 +480,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
         cp = (spv - 1.f) * A.inv_b;
         break;
     }
-    const float ap = score_alpha<SK>(cp, Rpv, lppv, tpv, A.pw);
+    const float ap = score_alpha<SK>(cp, Rpv, lppv, tpv, A.pw, A.p);
     float n[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) n[v] = ap * ap * mg[MG_UN + v];
@@ -526,7 +533,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
     for (int j = jbeg + lane; j < jend; j += KGE_WAVE) {
       const float R = gR[j];
       float lp;
-      const float s = score_value<SK>(R, A.pw, &lp);
+      const float s = score_value<SK>(R, A.pw, &lp, A.p);
       const int64_t q = i * Keff + j;
       switch (A.loss_kind) {
         case KGE_LOSS_HINGE: lfin += fmaxf(A.margin + s - spv, 0.f); break;
@@ -538,7 +545,10 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4)
       if (A.neg_score_out) A.neg_score_out[q] = s;
       if (A.train) {
         const float c = neg_coef(A, s, spv, Ms, invZ);
-        A.coef[((uint32_t)i << A.kshift) | (uint32_t)j] = make_float2(score_alpha<SK>(c, R, lp, gT[j], A.pw), R);
+        // .y: what the update kernel's gradient needs besides alpha (p = inf: the
+        // row maximum; general p: p itself)
+        A.coef[((uint32_t)i << A.kshift) | (uint32_t)j] =
+            make_float2(score_alpha<SK>(c, R, lp, gT[j], A.pw, A.p), SK == SK_PGEN ? A.p : R);
         bin_key(A, ids[j], ((uint32_t)i << A.kshift) | (uint32_t)j);
       }
     }
@@ -1021,6 +1031,7 @@ static kge_status by_sk(const StepArgs& A, const StepGeom& G, int sk, hipStream_
     case SK_P1: return launch_family<Model, VEC, NC, SK_P1>(A, G, st, ev);
     case SK_P2: return launch_family<Model, VEC, NC, SK_P2>(A, G, st, ev);
     case SK_PINF: return launch_family<Model, VEC, NC, SK_PINF>(A, G, st, ev);
+    case SK_PGEN: return launch_family<Model, VEC, NC, SK_PGEN>(A, G, st, ev);
     default: return launch_family<Model, VEC, NC, SK_DOT>(A, G, st, ev);
   }
 }
@@ -1031,6 +1042,7 @@ static kge_status by_sk_lp(const StepArgs& A, const StepGeom& G, int sk, hipStre
     case SK_P1: return launch_family<Model, VEC, NC, SK_P1>(A, G, st, ev);
     case SK_P2: return launch_family<Model, VEC, NC, SK_P2>(A, G, st, ev);
     case SK_PINF: return launch_family<Model, VEC, NC, SK_PINF>(A, G, st, ev);
+    case SK_PGEN: return launch_family<Model, VEC, NC, SK_PGEN>(A, G, st, ev);
     default: return KGE_EUNSUPPORTED;
   }
 }

@@ -47,6 +47,7 @@ template <int SK>
 __device__ __forceinline__ float lp_elem_grad(float a, float alpha, float M) {
   if (SK == SK_P2) return alpha * a;
   float s = a > 0.f ? alpha : (a < 0.f ? -alpha : 0.f);
+  if (SK == SK_PGEN) return a != 0.f ? s * powf(fabsf(a), M - 1.f) : 0.f;   // M carries p
   if (SK == SK_PINF && fabsf(a) != M) s = 0.f;
   return s;
 }
@@ -111,9 +112,9 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
   int64_t ph = load_idx(A.pos, i * 3 + 0, A.i64);
   int64_t pr = load_idx(A.pos, i * 3 + 1, A.i64);
   int64_t pt = load_idx(A.pos, i * 3 + 2, A.i64);
-  if (ph < 0 || ph >= A.ent.rows) { err = KGE_ERANGE; ph = 0; }
+  ph = ent_row(A, ph, &err);
   if (pr < 0 || pr >= A.rel.rows) { err = KGE_ERANGE; pr = 0; }
-  if (pt < 0 || pt >= A.ent.rows) { err = KGE_ERANGE; pt = 0; }
+  pt = ent_row(A, pt, &err);
   for (int j = tid; j < K; j += kTrThreads) ids[j] = slot_entity(A, i, j, &err);
   __syncthreads();
   auto row_id = [&](int q) -> int64_t { return q == 0 ? ph : q == 1 ? pt : (int64_t)ids[q - 2]; };
@@ -237,7 +238,8 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
         } else {
           const float a = x - y, ma = fabsf(a);
           av[v] = a;
-          part = SK == SK_P2 ? part + ma * ma : SK == SK_P1 ? part + ma : fmaxf(part, ma);
+          part = SK == SK_P2 ? part + ma * ma : SK == SK_P1 ? part + ma
+               : SK == SK_PGEN ? part + powf(ma, A.p) : fmaxf(part, ma);
         }
       }
     }
@@ -251,7 +253,7 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
       ties = wsum(tq);
     }
     float lp;
-    const float s = score_value<SK>(R, A.pw, &lp);
+    const float s = score_value<SK>(R, A.pw, &lp, A.p);
     if (lane == 0) { sS[q] = s; sR[q] = R; sT[q] = ties; }
   }
   __syncthreads();
@@ -275,9 +277,9 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
     for (int q = lane; q < K; q += KGE_WAVE) {
       const float s = sS[q];
       float lp;
-      score_value<SK>(sR[q], A.pw, &lp);
+      score_value<SK>(sR[q], A.pw, &lp, A.p);
       const float c = neg_coef(A, s, sp, Ms, invZ);
-      sA[q] = score_alpha<SK>(c, sR[q], lp, sT[q], A.pw);
+      sA[q] = score_alpha<SK>(c, sR[q], lp, sT[q], A.pw, A.p);
       csum += c;
       switch (A.loss_kind) {
         case KGE_LOSS_HINGE: lneg += fmaxf(A.margin + s - sp, 0.f); break;
@@ -302,8 +304,8 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
         default: lossp = ((sp - 1.f) * (sp - 1.f) + lneg) * 0.5f * A.inv_b; cp = (sp - 1.f) * A.inv_b; break;
       }
       float lpp;
-      score_value<SK>(sR[K], A.pw, &lpp);
-      sA[K] = score_alpha<SK>(cp, sR[K], lpp, sT[K], A.pw);
+      score_value<SK>(sR[K], A.pw, &lpp, A.p);
+      sA[K] = score_alpha<SK>(cp, sR[K], lpp, sT[K], A.pw, A.p);
       misc[0] = lossp;
       if (A.pos_score_out) A.pos_score_out[i] = sp;
     }
@@ -329,7 +331,7 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
       const int xr = xrow_of(q, kind), yr = yrow_of(q, kind);
       const float* xp = P + xr * LP;
       const float* yp = P + yr * LP;
-      const float alpha = sA[q], Mx = sR[q];
+      const float alpha = sA[q], Mx = SK == SK_PGEN ? A.p : sR[q];
       float gx[kTrKV], gy[kTrKV];
       float gxx = 0.f, dx = 0.f, dy = 0.f;
 #pragma unroll
@@ -626,6 +628,7 @@ kge_status launch_step_transr(const StepArgs& A, const StepGeom& G, const TrArgs
     case SK_P1: launch_tr<SK_P1>(A, G, T, P, st, ev); break;
     case SK_P2: launch_tr<SK_P2>(A, G, T, P, st, ev); break;
     case SK_PINF: launch_tr<SK_PINF>(A, G, T, P, st, ev); break;
+    case SK_PGEN: launch_tr<SK_PGEN>(A, G, T, P, st, ev); break;
     default: launch_tr<SK_DOT>(A, G, T, P, st, ev); break;
   }
   return KGE_OK;

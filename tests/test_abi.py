@@ -110,7 +110,7 @@ def test_workspace_query_valid_descriptor(lib):
     ("abi_version", 99, 1, "abi_version"),
     ("loss_kind", 9, 1, "loss kind"),
     ("dim", 5, 1, "columns"),
-    ("score_p", 3.0, 5, "p in"),
+    ("score_p", -1.0, 1, "p > 0"),
     ("negative_ratio", -1, 1, "negative_ratio"),
 ])
 def test_invalid_descriptors_are_rejected_without_gpu(lib, field, value, status, msg):

@@ -65,13 +65,13 @@ def test_rank_toy_matches_get_rank(name, side, tmp_path):
 
 
 @pytest.mark.parametrize("name,si", [("TransE", 1), ("TransE", 2), ("TransE", 3), ("TransH", 4), ("TransD", 5),
-                                     ("RotatE", 2), ("TransR", 3)])
+                                     ("RotatE", 2), ("TransR", 3), ("TransE", 6), ("RotatE", 6), ("TransD", 7)])
 def test_rank_score_kinds(name, si, tmp_path):
     """Every score kind the kernel instantiates (p = 1, 2, inf, Pow, Dot)."""
     from KGE import ranking, score
     train, val, md = toy()
     s = [score.LpDistance(2), score.LpDistance(1), score.LpDistance(np.inf), score.LpDistancePow(2),
-         score.LpDistancePow(1), score.Dot()][si]
+         score.LpDistancePow(1), score.Dot(), score.LpDistance(3), score.LpDistancePow(1.5)][si]
     m = build(name, s)
     m.train(train_X=train, val_X=val, metadata=md, epochs=1, batch_size=4, optimizer="SGD", seed=3,
             log_path=str(tmp_path))

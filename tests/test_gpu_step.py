@@ -281,6 +281,19 @@ def test_transd_matrix(hiplib, si, li):
     check(ref, got, l_, ps, ns)
 
 
+@pytest.mark.parametrize("model_name", ["TransE", "RotatE", "TransR", "TransH", "TransD"])
+@pytest.mark.parametrize("kind,p", [("lp", 3.0), ("lppow", 1.5), ("lp", 0.5)])
+@pytest.mark.parametrize("li", [0, 3])
+def test_general_p(hiplib, model_name, kind, p, li):
+    """LpDistance / LpDistancePow with p outside {1, 2, inf} (score.py:49-76)
+    on the fused kernels (SK_PGEN) vs the oracle."""
+    from KGE import score
+    s = (score.LpDistance if kind == "lp" else score.LpDistancePow)(p)
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, model_name, 24, 9, 6, "h+t", s, _losses()[li],
+                                          k=20 if model_name in ("TransR", "TransD") else None)
+    check(ref, got, l_, ps, ns)
+
+
 @pytest.mark.parametrize("model_name", ["TransH", "TransD"])
 @pytest.mark.parametrize("d,k,B,K,side,constraint", [(200, 200, 6, 64, "h+t", True), (32, 48, 17, 3, "t", True),
                                                       (40, 16, 9, 5, "h", False), (17, 33, 5, 70, "h+t", True),
