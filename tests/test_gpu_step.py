@@ -659,6 +659,49 @@ def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("model_name", ["TransE", "RotatE", "TransD", "TransR"])
+def test_gathered_shard_layout_remap(hiplib, model_name):
+    """The dense multi-GPU exchange's table layout on one GPU: the entity
+    rows laid out as G = 3 all-gathered shards (row (e mod 3) * Es + e div 3,
+    padded), kge_step given shard_count / shard_rows / global_entities draws
+    and maps global ids in-kernel; un-permuted rows == the oracle step."""
+    from KGE import engine, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    dev = _dev()
+    rng = np.random.default_rng(41)
+    E, R, d, B, K, G = 29, 4, 24, 10, 6, 3
+    k = 20 if model_name in ("TransR", "TransD") else None
+    W = _weights(model_name, E, R, d, rng, k)
+    Es = -(-E // G)
+    perm = np.array([(e % G) * Es + e // G for e in range(E)])
+
+    def gathered(x):
+        out = np.zeros((G * Es,) + x.shape[1:], np.float32)
+        out[perm] = x
+        return torch.tensor(out, device=dev)
+    sc = {"TransE": score.LpDistance(2), "RotatE": score.LpDistance(1)}.get(model_name, score.LpDistancePow(2))
+    m = _make(model_name, d, K, "h+t", sc, loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E, R,
+              UniformStrategy(np.arange(E), seed=13), constraint=False, k=k)
+    m.model_weights = {kk: (gathered(v) if kk in ("ent_emb", "ent_proj") else torch.tensor(v, device=dev))
+                       for kk, v in W.items()}
+    step = engine.FusedStep(m)
+    step.shard = (G, Es, E)
+    pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+    plane = m.ns_strategy.offset
+    step(torch.tensor(pos, device=dev), True, optimizers.SGD(0.05))
+    torch.cuda.synchronize()
+    step.check_status()
+    neg = orc.negatives(pos, K, "h+t", E, seed=13, plane=plane)
+    ref = orc.train_step(model_name, W, pos, neg, score=_spec_score(sc), loss=("sans", 3.0, 1.0), lr=0.05,
+                         constraint=False, limit=getattr(m, "limit", None))
+    assert abs(float(step.loss_out.item()) - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"]))
+    for kk, v in ref["weights"].items():
+        got = m.model_weights[kk].cpu().numpy()
+        if kk in ("ent_emb", "ent_proj"):
+            got = got[perm]
+        np.testing.assert_allclose(got, v, atol=TOL, err_msg=kk)
+
+
 def test_sharded_step_c5_shard_size(hiplib):
     """One GPU at the C5 per-rank shard size (6.25M rows x 512, TransE, K=256
     h+t, SANS) through the sparse exchange: finite loss, only touched rows

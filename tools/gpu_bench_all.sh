@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/$1
 shift
-LEGS=${@:-c1 c3 c4-rescal c4-transr c2-50m c2}
+LEGS=${@:-c1 c3 c4-rescal c4-transr c2-50m c5 c2}
 mkdir -p "$OUT"
 for w in $LEGS; do
   timeout -k 10 300 python -u bench.py --workload $w --no-cpu-baseline > "$OUT/bench_$w.json" 2> "$OUT/bench_$w.err" || { echo "bench $w failed"; tail -20 "$OUT/bench_$w.err"; exit 3; }
