@@ -25,7 +25,8 @@ FLAG_GRAD_ROWS_TOUCHED = 8
 RANK_TRANS, RANK_ROT, RANK_MUL, RANK_DOT = range(4)
 RPROJ_NONE, RPROJ_HYPER, RPROJ_RANK1 = range(3)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libkge_hip.so")
+LIB_PATH = os.environ.get("KGE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                                                      "libkge_hip.so")   # KGE_LIB: a tuning variant (tools/variants.py)
 
 
 class kge_table(ctypes.Structure):

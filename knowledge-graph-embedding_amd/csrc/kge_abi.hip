@@ -206,7 +206,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   // score kernel: wpp waves per positive so that a wave streams <= 64 slots;
   // 8 / wpp positives per workgroup
   int wpp = 1;
-  while (wpp < kMaxWpp && (int64_t)wpp * 64 < Keff) wpp <<= 1;
+  while (wpp < kMaxWpp && (int64_t)wpp * KGE_SLOTS_PER_WAVE < Keff) wpp <<= 1;
   const int nP = kStepWaves / wpp;
   // 'h+t': even slot ranges, so every stream batch starts on an h-corrupt slot
   int SW = std::max<int>(1, (int)ceil_div(Keff, wpp));

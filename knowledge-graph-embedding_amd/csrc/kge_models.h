@@ -234,6 +234,7 @@ struct MP {
 template <int VEC, int NC, int SK>
 struct TransE {
   static constexpr bool CPLX = false;
+  static constexpr bool WIDE = false;   // score kernel fits 128 VGPRs at one chunk (4 waves / SIMD)
   static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
@@ -383,6 +384,7 @@ struct TransE {
 template <int VEC, int NC, int SK_UNUSED>
 struct DistMult {
   static constexpr bool CPLX = false;
+  static constexpr bool WIDE = true;    // five context rows: 256-VGPR budget (2 waves / SIMD)
   static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
@@ -464,6 +466,7 @@ struct DistMult {
 template <int VEC, int NC, int SK>
 struct RotatE {
   static constexpr bool CPLX = true;
+  static constexpr bool WIDE = true;
   static constexpr bool MAT = false;
   static constexpr int NSNAP = 3;
   static constexpr int HV = VEC / 2;
@@ -597,6 +600,7 @@ struct RotatE {
 template <int VEC, int NC, int SK_UNUSED>
 struct Rescal {
   static constexpr bool CPLX = false;
+  static constexpr bool WIDE = false;
   static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
@@ -664,6 +668,7 @@ struct Rescal {
 template <int VEC, int NC, int SK_UNUSED>
 struct Materialised {
   static constexpr bool CPLX = false;
+  static constexpr bool WIDE = false;
   static constexpr bool MAT = true;
   static constexpr int NSNAP = 0;
   static constexpr bool NRM_FROM_R = false;

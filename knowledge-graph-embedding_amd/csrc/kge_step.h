@@ -10,6 +10,15 @@ constexpr int kStepThreads = kStepWaves * KGE_WAVE;
 constexpr int kUpdWaves = 4;       // waves per update workgroup (one destination row per wave)
 constexpr int kUpdThreads = kUpdWaves * KGE_WAVE;
 constexpr int kMaxWpp = 8;         // waves per positive, at most
+#ifndef KGE_SLOTS_PER_WAVE
+#define KGE_SLOTS_PER_WAVE 64      // score kernel: negative slots a wave streams, at most (tuning knob)
+#endif
+#ifndef KGE_SCORE_WPE
+#define KGE_SCORE_WPE 4            // score kernel: amdgpu_waves_per_eu (tuning knob)
+#endif
+#ifndef KGE_SCORE_WPE_WIDE
+#define KGE_SCORE_WPE_WIDE 2       // ... for rows of two or more fragment chunks (register room, no spills)
+#endif
 constexpr int kMergeStride = 32;   // floats of per-positive merge state in the score kernel's LDS
 constexpr int kSortMax = 1024;     // update kernel: longest destination list sorted in LDS (per wave)
 

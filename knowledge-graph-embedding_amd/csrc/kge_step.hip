@@ -26,7 +26,7 @@
 //                   positives' own row gradients added, clip scale and SGD
 //                   (BaseModel.py:328, keras SGD ResourceScatterAdd) applied
 //                   with ONE read-modify-write per touched row.
-#include "kge_step_impl.h"
+#include "kge_proj.h"
 
 namespace kge {
 
@@ -109,6 +109,11 @@ kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int mod
 }
 
 #ifdef KGE_ONLY_ONE
+// single-instance builds (tools/phase_prof.py, tools/variants.py): the other families are stubs
+kge_status launch_step_proj(const StepArgs&, const StepGeom&, const PjPlan&, int, hipStream_t, hipEvent_t const*) {
+  return KGE_EUNSUPPORTED;
+}
+kge_status launch_rank(const RankArgs&, int, int, int, hipStream_t) { return KGE_EUNSUPPORTED; }
 kge_status launch_step_rescal(const StepArgs&, const StepGeom&, const RelArgs&, float, float*, hipStream_t,
                               hipEvent_t const*) {
   return KGE_EUNSUPPORTED;

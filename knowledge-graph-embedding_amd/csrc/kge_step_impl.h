@@ -193,7 +193,7 @@ static_assert(MG_IZ < MG_STRIDE, "merge slots exceed the LDS stride");
 // finalises its slots' coefficients and files every destination key into
 // that destination's list for the update kernel.
 template <template <int, int, int> class Model, int VEC, int NC, int SK, int SIDE>
-__global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu(4))) void score_kernel(StepArgs A) {
+__global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((NC >= 2 || Model<VEC, NC, SK>::WIDE) ? KGE_SCORE_WPE_WIDE : KGE_SCORE_WPE))) void score_kernel(StepArgs A) {
   using M = Model<VEC, NC, SK>;
   using F = Frag<VEC, NC>;
   constexpr int W = kStepWaves;

@@ -1,0 +1,50 @@
+"""Score-kernel tuning variants (C2 instance only, -DKGE_ONLY_ONE).
+
+    python tools/variants.py build NAME -DKGE_SLOTS_PER_WAVE=128 ...   # here: KGE/_lib/libkge_var_NAME.so
+    python tools/variants.py run NAME [NAME ...]                        # on the GPU box: bench.py per variant
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "knowledge-graph-embedding_amd", "csrc")
+LIBDIR = os.path.join(ROOT, "knowledge-graph-embedding_amd", "KGE", "_lib")
+
+
+def build(name, defines):
+    objs, procs = [], []
+    for src in ("kge_step.hip", "kge_abi.hip", "kge_transr.hip", "kge_rel.hip"):
+        obj = "/tmp/var_%s_%s" % (name, src.replace(".hip", ".o"))
+        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DKGE_ONLY_ONE"] + defines + \
+              ["-c", os.path.join(CSRC, src), "-o", obj]
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    for p in procs:
+        assert p.wait() == 0
+    out = os.path.join(LIBDIR, "libkge_var_%s.so" % name)
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC"] + objs + ["-o", out], check=True)
+    print("built", out)
+
+
+def run(names):
+    import json
+    for n in names:
+        env = dict(os.environ, KGE_LIB=os.path.join(LIBDIR, "libkge_var_%s.so" % n))
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"], env=env,
+                             capture_output=True, text=True, timeout=300)
+        line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+        if not line:
+            print(n, "FAILED", out.stderr[-800:])
+            continue
+        d = json.loads(line[-1])
+        k = d["roofline"]["kernels"]
+        print("%-12s %.5f ms/step  KS %.5f  KU %.5f" % (n, d["ms_per_step"], k["score_kernel"]["ms"],
+                                                        k["update_kernel"]["ms"]), flush=True)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build(sys.argv[2], sys.argv[3:])
+    else:
+        run(sys.argv[2:])
