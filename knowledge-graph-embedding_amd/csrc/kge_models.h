@@ -550,13 +550,12 @@ struct RotatE {
     store_row(c.CS, sb + cols, cols);
     store_row(c.T, sb + 2 * cols, cols);
   }
+  // both rows loaded on every path (only the first one's address depends on
+  // the kind): a branch-free shape keeps the update kernel's per-entry
+  // contexts in registers (a half-filled struct array went to scratch)
   __device__ static void load_ectx(const float* sb, int cols, int kind, ECtx& ec) {
-    if (kind == KIND_TC) {
-      load_row(ec.c0, sb, cols);
-    } else {
-      load_row(ec.c0, sb + cols, cols);
-      load_row(ec.c1, sb + 2 * cols, cols);
-    }
+    load_row(ec.c0, sb + (kind == KIND_TC ? 0 : cols), cols);
+    load_row(ec.c1, sb + 2 * cols, cols);
   }
   __device__ static void grad_entity(const ECtx& ec, int kind, const F& E, float alpha, float M, F& gE) {
     if (kind == KIND_TC) {

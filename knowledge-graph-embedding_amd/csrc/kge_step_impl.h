@@ -691,8 +691,10 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
     int jj[U], cc[U];
     typename M::ECtx ec[U];   // a positive's own row gradient goes into ec[u].c0
     float2 cf[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
+    // compile-time entry indices (static_for): the per-entry context rows stay
+    // in registers (a runtime-indexed loop too large to unroll put them in scratch)
+    static_for<U>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
       if (u < cntv) {
         decode(codes[u], &ii[u], &jj[u], &cc[u]);
         if (cc[u] < 0) {
@@ -708,9 +710,9 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
           load_row(ec[u].c0, A.gpe + ii[u] * (int64_t)A.gpe_stride + (cc[u] == 0 ? 0 : A.gpe_toff), A.ent.cols);
         }
       }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
+    });
+    static_for<U>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
       if (u < cntv) {
         if (cc[u] < 0) {
           if constexpr (M::LINEAR_E) {
@@ -729,7 +731,7 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
           add_to(acc, ec[u].c0);
         }
       }
-    }
+    });
   };
   auto rel_add = [&](const uint32_t* codes, int cntv, float (&acc)[RV * NC]) {
     float g[U][RV * NC];
@@ -794,22 +796,22 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
               typename M::ECtx ec[U];
               float2 cf[U];
               int kd[U];
-#pragma unroll
-              for (int u = 0; u < U; ++u) {
+              static_for<U>([&](auto uc) {
+                constexpr int u = decltype(uc)::value;
                 const uint32_t code = code_at(min(p0 + u, nn - 1));
                 const uint32_t i = code >> A.kshift;
                 kd[u] = slot_kind(A.side_mode, (int)(code & kmask));
                 cf[u] = A.coef[code];
                 M::load_ectx(A.snap + i * snap_stride, A.snap_cols, kd[u], ec[u]);
-              }
-#pragma unroll
-              for (int u = 0; u < U; ++u) {
+              });
+              static_for<U>([&](auto uc) {
+                constexpr int u = decltype(uc)::value;
                 float aE, aC;
                 M::lin_coefs(kd[u], p0 + u < nn ? cf[u].x : 0.f, aE, aC);
                 accE += aE;
 #pragma unroll
                 for (int q = 0; q < VEC * NC; ++q) acc.v[q] += aC * ec[u].c0.v[q];
-              }
+              });
             }
             p0 = nn;
           }
