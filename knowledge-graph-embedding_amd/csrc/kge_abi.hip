@@ -332,7 +332,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.o_list = take((uint64_t)ndest * cap * 4);
   P.o_ovf = take((uint64_t)T * 8);
   P.o_upart = take((uint64_t)P.G.gridU * 4);
-  P.o_touched = take((uint64_t)(compact ? T : 1) * 4);
+  P.o_touched = take((uint64_t)(compact ? (int64_t)P.G.gridU * kUpdWaves : 1) * 8);
   if (rescal) {
     const int64_t nct = ceil_div(d->dim, 16);
     P.o_sorted = take((uint64_t)B * 4);
@@ -504,7 +504,7 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   A.list = (uint32_t*)(ws + P.o_list);
   A.ovf = (uint64_t*)(ws + P.o_ovf);
   A.upart = (float*)(ws + P.o_upart);
-  A.touched = (uint32_t*)(ws + P.o_touched);
+  A.touched = (uint2*)(ws + P.o_touched);
   A.gpe = A.gpos;
   A.gpe_stride = 3 * A.gcols;
   A.gpe_toff = 2 * A.gcols;

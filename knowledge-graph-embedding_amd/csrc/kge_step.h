@@ -78,10 +78,11 @@ struct StepArgs {
   float* upart;     // [gridU] update-kernel norm^2 partials (dense mode)
   float* gneg;      // materialised family: [B << kshift, ent.cols] negatives' entity-row gradients
   // compact update launch (tables much larger than a step's keys): the score
-  // pass appends each destination's first key to `touched`, and the update
-  // kernel visits only those rows (untouched rows are not read or written)
+  // pass appends each destination and its first key's code to `touched`, and
+  // the update kernel visits only those rows (untouched rows are not read or
+  // written)
   bool compact;
-  uint32_t* touched;
+  uint2* touched;
   // multi-table update passes (TransH / TransD): the aux-table pass runs
   // first over the same destination lists and leaves the counters for the
   // main pass; scale[] slots of the pass's entity / relation variable

@@ -121,7 +121,7 @@ __device__ __forceinline__ float neg_coef(const StepArgs& A, float s, float sp, 
 // order), or to the overflow list once that list is full
 __device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_t code) {
   const uint32_t r = atomicAdd(&A.cnt[dest], 1u);
-  if (A.compact && r == 0u) A.touched[atomicAdd(&A.ctl->ntouched, 1u)] = (uint32_t)dest;
+  if (A.compact && r == 0u) A.touched[atomicAdd(&A.ctl->ntouched, 1u)] = make_uint2((uint32_t)dest, code);
   if (r < (uint32_t)A.cap) {
     A.list[dest * A.cap + r] = code;
   } else {
@@ -660,9 +660,13 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
   const int64_t dd = (int64_t)blockIdx.x * kUpdWaves + wv;
   int64_t d;
   bool active;
+  uint32_t code1 = 0xFFFFFFFFu;   // compact: the destination's first filed code
   if (A.compact) {   // only the destinations this step touched
+    // read unconditionally (the array is padded to the grid), with the length
+    const uint2 t = A.touched[dd];
     active = dd < (int64_t)A.ctl->touched_len;
-    d = active ? (int64_t)A.touched[dd] : 0;
+    d = active ? (int64_t)t.x : 0;
+    code1 = t.y;
   } else {
     active = dd < (A.rel_only ? R_ : ndest);
     d = dd < R_ ? E_ + dd : dd - R_;
@@ -763,9 +767,26 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
     F E, acc;
     acc.zero();
     E.zero();
+    // compact launches over large tables: most destinations hold exactly one
+    // key, whose code came with the destination -- its coefficient and context
+    // row are requested together with the counter (used when n == 1)
+    const bool pre = A.compact && is_ent && code1 < nneg;
+    typename M::ECtx ec1;
+    float2 cf1 = make_float2(0.f, 0.f);
+    int kd1 = 0;
+    if (pre) {
+      kd1 = slot_kind(A.side_mode, (int)(code1 & kmask));
+      if constexpr (M::MAT) {
+        load_row(ec1.c0, A.gneg + (int64_t)code1 * A.ent.cols, A.ent.cols);
+      } else {
+        cf1 = A.coef[code1];
+        M::load_ectx(A.snap + (code1 >> A.kshift) * snap_stride, A.snap_cols, kd1, ec1);
+      }
+    }
     // an untouched row is read only when the step rewrites it anyway (fused
-    // constraint) or it carries a dense term
-    if (is_ent && (n != 0u || A.fuse_norm || A.dense)) {
+    // constraint) or it carries a dense term; a compact launch visits only
+    // touched rows (issued without waiting for the counter)
+    if (is_ent && (A.compact || n != 0u || A.fuse_norm || A.dense)) {
       load_row(E, A.ent.row(d), A.ent.cols);
       if (A.fuse_norm) {
         normalize_row(E);   // the step's constraint assign, then this step's update
@@ -826,6 +847,19 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
       };
       if (n == 0u) {
         // dense mode, untouched row: the regulariser term only
+      } else if (pre && n == 1u) {
+        // the single (negative) key, context already in registers
+        if constexpr (M::LINEAR_E) {
+          float aE, aC;
+          M::lin_coefs(kd1, cf1.x, aE, aC);
+          accE += aE;
+#pragma unroll
+          for (int q = 0; q < VEC * NC; ++q) acc.v[q] += aC * ec1.c0.v[q];
+        } else {
+          F g;
+          M::grad_entity(ec1, kd1, E, cf1.x, cf1.y, g);
+          add_to(acc, g);
+        }
       } else if (n <= (uint32_t)A.cap && n <= (uint32_t)KGE_WAVE) {
         // ascending code order: each code's rank among the n (codes are
         // unique), then a forward permute puts code of rank r in lane r
