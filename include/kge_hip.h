@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KGE_ABI_VERSION 3
+#define KGE_ABI_VERSION 4
 
 typedef enum kge_status {
   KGE_OK = 0,
@@ -322,6 +322,34 @@ typedef struct kge_apply_rows_desc {
 } kge_apply_rows_desc;
 
 kge_status kge_apply_rows(const kge_apply_rows_desc* d, void* stream);
+
+/* Device-resident input stream (§8 f2; replaces data_utils.py:176-196's
+ * tf.data shuffle -> repeat -> batch): batch rows [start, start + batch) of
+ * the endless stream over a resident [n_rows, 3] triple array. Stream
+ * position p is row pi_e(p mod n_rows) of epoch e = p div n_rows, so a batch
+ * straddles epochs exactly like repeat().batch(). With shuffle = 0 pi_e is
+ * the identity; otherwise it is a fresh permutation per epoch
+ * (reshuffle_each_iteration): a 4-round balanced Feistel network on w-bit
+ * values (w = the smallest even width >= 2 with 2^w >= n_rows, halves of
+ * h = w/2 bits), round r of (L, R) -> (R, L ^ F_r(R)) with
+ * F_r(R) = word 0 of Philox4x32-10(counter = (R, r, e lo, e hi),
+ * key = (seed lo, seed hi)) masked to h bits, cycle-walked (re-applied while
+ * the value is >= n_rows) so that it permutes [0, n_rows). No permutation is
+ * stored: each output row computes its own source row. */
+typedef struct kge_stream_desc {
+  int32_t abi_version;        /* KGE_ABI_VERSION                                */
+  int32_t idx_dtype;          /* KGE_IDX_* of triples and out                   */
+  const void* triples;        /* [n_rows, 3], device-resident                   */
+  int64_t n_rows;             /* > 0                                            */
+  int64_t start;              /* stream position of the batch's first row, >= 0 */
+  int64_t batch;              /* rows to produce, >= 0                          */
+  uint64_t seed;
+  int32_t shuffle;            /* 0: epoch order, 1: per-epoch permutation       */
+  int32_t _pad;
+  void* out;                  /* [batch, 3] idx_dtype                           */
+} kge_stream_desc;
+
+kge_status kge_stream_batch(const kge_stream_desc* d, void* stream);
 
 /* ABI version compiled into the library. */
 int32_t kge_abi_version(void);

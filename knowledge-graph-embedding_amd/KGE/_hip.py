@@ -11,7 +11,7 @@ import threading
 
 import torch
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 KGE_OK, KGE_EINVAL, KGE_ERANGE, KGE_EHIP, KGE_ENOMEM_WORKSPACE, KGE_EUNSUPPORTED = range(6)
 
@@ -99,8 +99,15 @@ class kge_apply_rows_desc(ctypes.Structure):
                 ("clip_norm", ctypes.c_float)]
 
 
+class kge_stream_desc(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("idx_dtype", ctypes.c_int32), ("triples", ctypes.c_void_p),
+                ("n_rows", ctypes.c_int64), ("start", ctypes.c_int64), ("batch", ctypes.c_int64),
+                ("seed", ctypes.c_uint64), ("shuffle", ctypes.c_int32), ("_pad", ctypes.c_int32),
+                ("out", ctypes.c_void_p)]
+
+
 EXPORTS = ("kge_abi_version", "kge_last_error", "kge_step_workspace_bytes", "kge_step", "kge_sample",
-           "kge_apply", "kge_constrain_rows", "kge_rank", "kge_apply_rows")
+           "kge_apply", "kge_constrain_rows", "kge_rank", "kge_apply_rows", "kge_stream_batch")
 
 _lock = threading.Lock()
 _lib = None
@@ -131,6 +138,8 @@ def load(path=LIB_PATH):
         L.kge_apply_rows.argtypes = [ctypes.POINTER(kge_apply_rows_desc), ctypes.c_void_p]
         L.kge_rank.restype = ctypes.c_int
         L.kge_rank.argtypes = [ctypes.POINTER(kge_rank_desc), ctypes.c_void_p]
+        L.kge_stream_batch.restype = ctypes.c_int
+        L.kge_stream_batch.argtypes = [ctypes.POINTER(kge_stream_desc), ctypes.c_void_p]
         L.kge_constrain_rows.restype = ctypes.c_int
         L.kge_constrain_rows.argtypes = [kge_table, ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]
         if L.kge_abi_version() != ABI_VERSION:

@@ -1,4 +1,5 @@
-"""Host (numpy) implementation of the counter-based negative-draw spec.
+"""Host (numpy) implementation of the counter-based negative-draw and
+input-stream specs.
 
 Used only by the eager plugin path on CPU tensors; CUDA tensors are sampled
 by ``kge_sample`` / the fused step in ``libkge_hip.so``. The spec (see
@@ -47,3 +48,40 @@ def draw(seed, plane, n, i64, rng):
         return (bits % np.asarray(rng, dtype=np.uint64)).astype(np.int64)
     bits = np.take_along_axis(w, q[..., None], -1)[..., 0]
     return (bits % np.asarray(rng, dtype=np.uint64)).astype(np.int64)
+
+
+def _feistel_pass(x, h, seed, epoch):
+    mask = np.uint64((1 << h) - 1)
+    L, R = x >> np.uint64(h), x & mask
+    for r in range(4):
+        w = philox4x32_10(R, np.uint64(r), np.uint64(epoch & 0xFFFFFFFF), np.uint64((epoch >> 32) & 0xFFFFFFFF),
+                          seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)[0]
+        L, R = R, (L ^ w) & mask
+    return (L << np.uint64(h)) | R
+
+
+def stream_rows(n, seed, start, batch, shuffle):
+    """Source rows of stream positions [start, start + batch) over n rows
+    (``kge_stream_desc`` in include/kge_hip.h): epoch e = p // n, row
+    pi_e(p % n), pi_e a cycle-walked 4-round Philox-keyed Feistel permutation
+    (the identity when not shuffling)."""
+    n = int(n)
+    p = np.arange(int(start), int(start) + int(batch), dtype=np.uint64)
+    k = p % np.uint64(n)
+    if not shuffle or len(p) == 0:
+        return k.astype(np.int64)
+    w = 2
+    while w < 64 and (1 << w) < n:
+        w += 2
+    h = w // 2
+    e = p // np.uint64(n)
+    out = np.empty_like(k)
+    for ep in np.unique(e):
+        sel = e == ep
+        y = _feistel_pass(k[sel], h, int(seed), int(ep))
+        bad = y >= np.uint64(n)
+        while bad.any():
+            y[bad] = _feistel_pass(y[bad], h, int(seed), int(ep))
+            bad = y >= np.uint64(n)
+        out[sel] = y
+    return out.astype(np.int64)

@@ -106,11 +106,13 @@ def calculate_data_size(X):
 
 
 def load_triples(data):
-    """numpy / tensor / CSV folder -> host int tensor [n, 3].
+    """numpy / tensor / ``.npy`` file / CSV folder -> host int tensor [n, 3].
 
     CSV folders are read as int32 (the reference's CsvDataset defaults,
     ``data_utils.py:182``); arrays keep an integer dtype (numpy default int64).
     """
+    if isinstance(data, str) and data.endswith(".npy") and os.path.isfile(data):
+        data = np.load(data, allow_pickle=False)
     if isinstance(data, str):
         parts = [pd.read_csv(os.path.join(data, f), header=None, dtype=np.int32).values
                  for f in sorted(os.listdir(data))]
@@ -127,53 +129,68 @@ def load_triples(data):
 
 
 class DeviceBatcher:
-    """Device-resident ``shuffle -> repeat -> batch`` stream.
+    """Device-resident ``shuffle -> repeat -> batch`` stream (SURVEY §8 f2).
 
-    The triples live on ``device``; each epoch draws a fresh permutation from a
-    host generator seeded once with ``seed`` (reshuffle_each_iteration), and
-    ``next()`` returns the next ``batch_size`` rows of the endless stream, so a
-    batch may span two epochs exactly like ``repeat().batch()``.
+    The triples stay resident on ``device``. Batch ``b`` is stream positions
+    ``[b B, (b + 1) B)``; position ``p`` is row ``pi_e(p mod n)`` of epoch
+    ``e = p div n``, so every batch has exactly ``batch_size`` rows and
+    batches straddle epochs like ``repeat().batch()``. ``pi_e`` is a fresh
+    permutation per epoch when shuffling (``reshuffle_each_iteration``): the
+    stateless Philox-keyed Feistel permutation of ``kge_stream_desc``
+    (``include/kge_hip.h``), computed per output row on the GPU by
+    ``kge_stream_batch`` -- no permutation array, no host work per batch. On a
+    CPU device the same rows come from the numpy restatement in
+    ``_philox.stream_rows``. tf.data's buffered shuffle order itself is not
+    reproducible (TF is not installed); the stream semantics are.
     """
 
     def __init__(self, data, batch_size, shuffle, seed=None, device=None):
         host = load_triples(data)
+        if host.dtype not in (torch.int32, torch.int64):
+            host = host.to(torch.int64)
         self.n = host.shape[0]
         if self.n == 0:
             raise ValueError("empty triple set")
         self.batch_size = int(batch_size)
-        self.shuffle = shuffle
+        if self.batch_size <= 0:
+            raise ValueError("batch_size must be > 0")
+        self.shuffle = bool(shuffle)
         self.device = device if device is not None else torch.device("cpu")
-        self.data = host.to(self.device)
-        self.gen = torch.Generator()
-        if seed is not None:
-            self.gen.manual_seed(int(seed))
-        else:
-            self.gen.seed()
-        self._order = None
-        self._pos = 0
-
-    def _next_epoch(self):
-        if self.shuffle:
-            perm = torch.randperm(self.n, generator=self.gen)
-        else:
-            perm = torch.arange(self.n)
-        self._order = perm.to(self.device)
-        self._pos = 0
+        self.data = host.contiguous().to(self.device)
+        self.seed = int(seed) if seed is not None else int.from_bytes(os.urandom(8), "little")
+        self.seed &= (1 << 64) - 1
+        self._pos = 0   # stream position of the next batch's first row
 
     def __iter__(self):
         return self
 
+    def rows(self, start, count):
+        """Source row indices of stream positions [start, start + count) (host int64)."""
+        from ._philox import stream_rows
+        return stream_rows(self.n, self.seed, start, count, self.shuffle)
+
     def __next__(self):
-        pieces = []
-        need = self.batch_size
-        while need > 0:
-            if self._order is None or self._pos >= self.n:
-                self._next_epoch()
-            take = min(need, self.n - self._pos)
-            pieces.append(self._order[self._pos:self._pos + take])
-            self._pos += take
-            need -= take
-        idx = pieces[0] if len(pieces) == 1 else torch.cat(pieces)
+        start, B = self._pos, self.batch_size
+        self._pos += B
+        if self.data.is_cuda:
+            import ctypes
+            from . import _hip
+            L = _hip.load()
+            out = torch.empty((B, 3), dtype=self.data.dtype, device=self.data.device)
+            d = _hip.kge_stream_desc()
+            d.abi_version = _hip.ABI_VERSION
+            d.idx_dtype = _hip.IDX_I64 if self.data.dtype == torch.int64 else _hip.IDX_I32
+            d.triples = self.data.data_ptr()
+            d.n_rows = self.n
+            d.start = start
+            d.batch = B
+            d.seed = self.seed
+            d.shuffle = 1 if self.shuffle else 0
+            d.out = out.data_ptr()
+            stream = torch.cuda.current_stream(self.data.device).cuda_stream
+            _hip.check(L.kge_stream_batch(ctypes.byref(d), ctypes.c_void_p(stream)), "kge_stream_batch")
+            return out
+        idx = torch.from_numpy(self.rows(start, B))
         return self.data.index_select(0, idx)
 
 

@@ -203,10 +203,12 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   if (proj && ncp > 2)
     return fail(KGE_EUNSUPPORTED, "row of %lld floats exceeds the projection kernel's %d", (long long)rowlen, 128 * vec);
 
-  // score kernel: wpp waves per positive so that a wave streams <= 64 slots;
-  // 8 / wpp positives per workgroup
+  // score kernel: wpp waves per positive -- the smallest divisor of the
+  // workgroup's waves that keeps a wave's share within KGE_SLOTS_PER_WAVE
+  // slots, else the whole workgroup -- and kStepWaves / wpp positives per
+  // workgroup
   int wpp = 1;
-  while (wpp < kMaxWpp && (int64_t)wpp * KGE_SLOTS_PER_WAVE < Keff) wpp <<= 1;
+  while (wpp < kStepWaves && ((int64_t)wpp * KGE_SLOTS_PER_WAVE < Keff || kStepWaves % wpp != 0)) ++wpp;
   const int nP = kStepWaves / wpp;
   // 'h+t': even slot ranges, so every stream batch starts on an h-corrupt slot
   int SW = std::max<int>(1, (int)ceil_div(Keff, wpp));
@@ -473,6 +475,24 @@ kge_status kge_apply(const kge_apply_desc* d, void* stream) {
                      (int32_t)t.cols, t.ld, d->grad, d->norm2, d->lr, d->clip_norm, adam ? 1 : 0, d->m, d->v,
                      d->beta_1, d->beta_2, d->epsilon, (float)lr_t);
   return hip_check("kge_apply");
+}
+
+kge_status kge_stream_batch(const kge_stream_desc* d, void* stream) {
+  if (!d) return fail(KGE_EINVAL, "null descriptor");
+  if (d->abi_version != KGE_ABI_VERSION)
+    return fail(KGE_EINVAL, "abi_version %d != library %d", d->abi_version, KGE_ABI_VERSION);
+  if (d->idx_dtype != KGE_IDX_I32 && d->idx_dtype != KGE_IDX_I64)
+    return fail(KGE_EINVAL, "kge_stream_batch: idx_dtype must be KGE_IDX_I32 or KGE_IDX_I64");
+  if (d->n_rows <= 0) return fail(KGE_EINVAL, "kge_stream_batch: n_rows must be > 0 (empty triple set)");
+  if (d->start < 0 || d->batch < 0) return fail(KGE_EINVAL, "kge_stream_batch: start and batch must be >= 0");
+  if (d->n_rows > (int64_t)1 << 62) return fail(KGE_ERANGE, "kge_stream_batch: n_rows exceeds 2^62");
+  if (d->batch == 0) return KGE_OK;
+  if (d->start > INT64_MAX - d->batch) return fail(KGE_ERANGE, "kge_stream_batch: stream position overflows");
+  if (!d->triples || !d->out) return fail(KGE_EINVAL, "kge_stream_batch: null triples / out");
+  if (d->shuffle != 0 && d->shuffle != 1) return fail(KGE_EINVAL, "kge_stream_batch: shuffle must be 0 or 1");
+  launch_stream(d->triples, d->idx_dtype == KGE_IDX_I64, d->n_rows, d->start, d->batch, d->seed, d->shuffle, d->out,
+                (hipStream_t)stream);
+  return hip_check("kge_stream_batch");
 }
 
 int32_t kge_abi_version(void) { return KGE_ABI_VERSION; }

@@ -5,11 +5,14 @@
 
 namespace kge {
 
-constexpr int kStepWaves = 8;      // waves per score workgroup
+#ifndef KGE_STEP_WAVES
+#define KGE_STEP_WAVES 8           // waves per score workgroup (tuning knob)
+#endif
+constexpr int kStepWaves = KGE_STEP_WAVES;
 constexpr int kStepThreads = kStepWaves * KGE_WAVE;
 constexpr int kUpdWaves = 4;       // waves per update workgroup (one destination row per wave)
 constexpr int kUpdThreads = kUpdWaves * KGE_WAVE;
-constexpr int kMaxWpp = 8;         // waves per positive, at most
+constexpr int kMaxWpp = kStepWaves > 8 ? kStepWaves : 8;   // waves per positive, at most
 #ifndef KGE_SLOTS_PER_WAVE
 #define KGE_SLOTS_PER_WAVE 64      // score kernel: negative slots a wave streams, at most (tuning knob)
 #endif
@@ -19,7 +22,7 @@ constexpr int kMaxWpp = 8;         // waves per positive, at most
 #ifndef KGE_SCORE_WPE_WIDE
 #define KGE_SCORE_WPE_WIDE 2       // ... for rows of two or more fragment chunks (register room, no spills)
 #endif
-constexpr int kMergeStride = 32;   // floats of per-positive merge state in the score kernel's LDS
+constexpr int kMergeStride = kMaxWpp + 24;   // floats of per-positive merge state in the score kernel's LDS
 constexpr int kSortMax = 1024;     // update kernel: longest destination list sorted in LDS (per wave)
 
 // Control block at the head of the workspace. The caller zero-fills the
@@ -249,6 +252,8 @@ struct RankArgs {
 };
 
 kge_status launch_rank(const RankArgs& A, int mode, int proj, int sk, hipStream_t st);
+void launch_stream(const void* tri, bool i64, int64_t n, int64_t start, int64_t batch, uint64_t seed, int shuffle,
+                   void* out, hipStream_t st);
 
 __global__ void constrain_rows_kernel(float* t, int64_t rows, int32_t cols, int64_t ld, int kind,
                                       float value);

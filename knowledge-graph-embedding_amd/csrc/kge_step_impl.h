@@ -176,8 +176,9 @@ __host__ __device__ constexpr int kind_at(int u) {
 }
 
 // per-positive merge slots (LDS)
-enum { MG_F = 0, MG_AP = 8, MG_LOSS = 9, MG_N = 10, MG_UN = 16, MG_RP = 20, MG_TP = 21, MG_SP = 22, MG_LPP = 23,
-       MG_RSQ = 24, MG_MS = 25, MG_IZ = 26, MG_STRIDE = kMergeStride };
+enum { MG_F = 0, MG_AP = kMaxWpp, MG_LOSS = kMaxWpp + 1, MG_N = kMaxWpp + 2, MG_UN = kMaxWpp + 8,
+       MG_RP = kMaxWpp + 12, MG_TP = kMaxWpp + 13, MG_SP = kMaxWpp + 14, MG_LPP = kMaxWpp + 15,
+       MG_RSQ = kMaxWpp + 16, MG_MS = kMaxWpp + 17, MG_IZ = kMaxWpp + 18, MG_STRIDE = kMergeStride };
 static_assert(MG_IZ < MG_STRIDE, "merge slots exceed the LDS stride");
 
 // ------------------------------------------------------------ KS score

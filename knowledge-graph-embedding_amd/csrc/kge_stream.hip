@@ -1,0 +1,68 @@
+// Device-resident input stream for gfx950: the batches of
+// data_utils.py:176-196's tf.data pipeline
+//   from_tensor_slices / CsvDataset -> shuffle(n, seed,
+//   reshuffle_each_iteration=True) -> repeat() -> batch(B)
+// produced on the device from the resident triple array, one launch per
+// batch and no host work: output row b is stream position p = start + b,
+// i.e. row pi_e(p mod n) of epoch e = p div n (batches straddle epochs as
+// repeat().batch() does). pi_e is a stateless per-epoch permutation -- a
+// 4-round Feistel network keyed by Philox4x32-10 and cycle-walked onto
+// [0, n) (include/kge_hip.h kge_stream_desc) -- so no permutation array is
+// built, stored or copied. Integer work only: one thread per output row.
+#include "kge_step.h"
+
+namespace kge {
+
+// one Feistel pass over w = 2h bits
+__device__ __forceinline__ uint64_t feistel_pass(uint64_t x, int h, PhiloxKey key, uint64_t epoch) {
+  const uint64_t mask = (h >= 32) ? 0xFFFFFFFFull : ((1ull << h) - 1ull);
+  uint64_t L = x >> h, R = x & mask;
+#pragma unroll
+  for (uint32_t r = 0; r < 4; ++r) {
+    const uint4 w = philox4x32_10(make_uint4((uint32_t)R, r, (uint32_t)epoch, (uint32_t)(epoch >> 32)), key);
+    const uint64_t nl = R;
+    R = (L ^ (uint64_t)w.x) & mask;
+    L = nl;
+  }
+  return (L << h) | R;
+}
+
+// pi_epoch(k) on [0, n): cycle-walk the w-bit permutation (terminates: k's
+// cycle returns to k < n)
+__device__ __forceinline__ uint64_t stream_perm(uint64_t k, uint64_t n, int h, PhiloxKey key, uint64_t epoch) {
+  uint64_t y = feistel_pass(k, h, key, epoch);
+  while (y >= n) y = feistel_pass(y, h, key, epoch);
+  return y;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void stream_batch_kernel(const T* __restrict__ tri, int64_t n, int64_t start,
+                                                           int64_t batch, int h, PhiloxKey key, int shuffle,
+                                                           T* __restrict__ out) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  const uint64_t p = (uint64_t)(start + b);
+  const uint64_t e = p / (uint64_t)n, k = p % (uint64_t)n;
+  const uint64_t row = shuffle ? stream_perm(k, (uint64_t)n, h, key, e) : k;
+  const T* src = tri + row * 3;
+  T* dst = out + b * 3;
+  dst[0] = src[0];
+  dst[1] = src[1];
+  dst[2] = src[2];
+}
+
+void launch_stream(const void* tri, bool i64, int64_t n, int64_t start, int64_t batch, uint64_t seed, int shuffle,
+                   void* out, hipStream_t st) {
+  int w = 2;
+  while (w < 64 && (1ull << w) < (uint64_t)n) w += 2;
+  const PhiloxKey key{(uint32_t)seed, (uint32_t)(seed >> 32)};
+  const unsigned blocks = (unsigned)((batch + 255) / 256);
+  if (i64)
+    hipLaunchKernelGGL(stream_batch_kernel<int64_t>, dim3(blocks), dim3(256), 0, st, (const int64_t*)tri, n, start,
+                       batch, w / 2, key, shuffle, (int64_t*)out);
+  else
+    hipLaunchKernelGGL(stream_batch_kernel<int32_t>, dim3(blocks), dim3(256), 0, st, (const int32_t*)tri, n, start,
+                       batch, w / 2, key, shuffle, (int32_t*)out);
+}
+
+}  // namespace kge

@@ -10,6 +10,8 @@ What it restates (reference = melissakou/knowledge-graph-embedding, TF 2.5):
     ``tests/golden/philox_kat.json``) in the corruption layout of
     ``BaseModel.py:332-408`` (h-side draws, then t-side; 'h+t' rows
     alternate h-corrupt / t-corrupt per positive);
+  * the input stream: ``data_utils.py:176-196``'s shuffle -> repeat ->
+    batch under the per-epoch permutation spec of ``kge_stream_desc``;
   * typed draws: ``utils.py:11-16`` (pool of the entity's type minus the
     entity) mapped from the same counter stream;
   * the step ``BaseModel.py:316-328``: constraint assigns, scores
@@ -156,6 +158,37 @@ def corrupt(pos, neg_ids, K, side):
         rep[hmask, 0] = neg_ids[hmask]
         rep[~hmask, 2] = neg_ids[~hmask]
     return rep
+
+
+# ---------------------------------------------------------------- input stream
+def stream_rows(n, seed, start, batch, shuffle):
+    """Source rows of stream positions [start, start + batch): the
+    ``shuffle(n, seed, reshuffle_each_iteration=True).repeat().batch()``
+    stream of ``data_utils.py:176-196`` under the per-epoch permutation spec
+    of ``kge_stream_desc`` (include/kge_hip.h), one position at a time with
+    the scalar Philox above. Small cases only (pure Python)."""
+    w = 2
+    while w < 64 and (1 << w) < n:
+        w += 2
+    h = w // 2
+    mask = (1 << h) - 1
+
+    def feistel(x, epoch):
+        L, R = x >> h, x & mask
+        for r in range(4):
+            f = philox4x32_10((R, r, epoch & 0xFFFFFFFF, epoch >> 32), (seed & 0xFFFFFFFF, seed >> 32))[0]
+            L, R = R, (L ^ f) & mask
+        return (L << h) | R
+
+    out = []
+    for p in range(start, start + batch):
+        e, k = divmod(p, n)
+        if shuffle:
+            k = feistel(k, e)
+            while k >= n:
+                k = feistel(k, e)
+        out.append(k)
+    return out
 
 
 # ---------------------------------------------------------------- scores / losses

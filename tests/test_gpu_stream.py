@@ -1,0 +1,91 @@
+"""GPU: the device input stream (kge_stream_batch, csrc/kge_stream.hip; SURVEY
+§8 f2, data_utils.py:176-196) against the oracle's scalar restatement at small
+sizes, the host numpy restatement at FB15k-237 size, and size-independent
+properties at full size (every epoch a permutation; batches = data rows).
+Integer work: bit-exact."""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import kge_oracle as O
+
+pytestmark = pytest.mark.gpu
+SEED = 0x0123456789ABCDEF
+
+
+@pytest.fixture(autouse=True)
+def _gpu(hiplib):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _stream(data, start, batch, shuffle, seed=SEED):
+    import ctypes
+    from KGE import _hip
+    L = _hip.load()
+    out = torch.full((batch, 3), -1, dtype=data.dtype, device=data.device)
+    d = _hip.kge_stream_desc()
+    d.abi_version = _hip.ABI_VERSION
+    d.idx_dtype = _hip.IDX_I64 if data.dtype == torch.int64 else _hip.IDX_I32
+    d.triples = data.data_ptr()
+    d.n_rows = data.shape[0]
+    d.start = start
+    d.batch = batch
+    d.seed = seed
+    d.shuffle = shuffle
+    d.out = out.data_ptr()
+    _hip.check(L.kge_stream_batch(ctypes.byref(d), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+               "kge_stream_batch")
+    torch.cuda.synchronize()
+    return out
+
+
+def _triples(n, dtype):
+    return (torch.arange(n * 3, dtype=torch.int64).reshape(n, 3) % (2 ** 31 - 1)).to(dtype).cuda()
+
+
+@pytest.mark.parametrize("dtype", [torch.int32, torch.int64])
+@pytest.mark.parametrize("n", [1, 2, 7, 64, 1001])
+@pytest.mark.parametrize("shuffle", [0, 1])
+def test_stream_matches_oracle(dtype, n, shuffle):
+    data = _triples(n, dtype)
+    for start in (0, n - 1, 5 * n + 3):
+        cnt = min(3 * n + 5, 600)
+        out = _stream(data, start, cnt, shuffle)
+        rows = torch.tensor(O.stream_rows(n, SEED, start, cnt, shuffle), device="cuda")
+        assert torch.equal(out, data[rows])
+
+
+def test_stream_fb15k237_size_matches_host():
+    """272,115 rows (FB15k-237 train), a 2^20-row batch straddling 4 epochs."""
+    from KGE import _philox
+    n = 272115
+    data = _triples(n, torch.int64)
+    start = 5 * n - 7
+    out = _stream(data, start, 1 << 20, 1)
+    rows = torch.from_numpy(_philox.stream_rows(n, SEED, start, 1 << 20, 1)).cuda()
+    assert torch.equal(out, data[rows])
+
+
+def test_stream_full_size_epoch_is_permutation():
+    """3,000,017 rows: one epoch's source rows (column 0 / 3) sort to 0..n-1,
+    the next epoch's differ."""
+    n = 3_000_017
+    data = _triples(n, torch.int64)
+    e2 = _stream(data, 2 * n, n, 1)[:, 0] // 3
+    assert torch.equal(torch.sort(e2).values, torch.arange(n, device="cuda"))
+    e3 = _stream(data, 3 * n, n, 1)[:, 0] // 3
+    assert not torch.equal(e2, e3)
+    assert torch.equal(_stream(data, 2 * n + 11, 1000, 0)[:, 0] // 3, torch.arange(11, 1011, device="cuda"))
+
+
+def test_device_batcher_matches_cpu_batcher():
+    from KGE.data_utils import set_tf_iterator
+    X = np.random.default_rng(0).integers(0, 1000, (1234, 3))
+    gpu = set_tf_iterator(X, 500, shuffle=True, buffer_size=len(X), seed=9, device=torch.device("cuda", 0))
+    cpu = set_tf_iterator(X, 500, shuffle=True, buffer_size=len(X), seed=9)
+    for _ in range(6):   # 3000 rows: straddles two epoch boundaries
+        g = next(gpu)
+        assert g.is_cuda and g.dtype == torch.int64
+        assert torch.equal(g.cpu(), next(cpu))
