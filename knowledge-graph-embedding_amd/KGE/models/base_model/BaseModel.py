@@ -97,6 +97,7 @@ class KGEModel:
                 logging.info("epoch: %i, train loss: %f, valid loss: %f" % (i, train_loss, val_loss))
             else:
                 logging.info("epoch: %i, train loss: %f" % (i, train_loss))
+            self._log_embeddings_histogram(i)
 
             if early_stopping_rounds is not None:
                 assert val_X is not None, "val_X should be given if want to check early stopping."
@@ -290,6 +291,33 @@ class KGEModel:
         os.makedirs(path, exist_ok=True)
         with open(os.path.join(path, "loss.jsonl"), "a") as f:
             f.write(json.dumps({"step": step, "loss": value}) + "\n")
+
+    def _log_embeddings_histogram(self, step, bucket_count=30):
+        """``tf.summary.histogram`` of every weight each epoch (``BaseModel.py:162,470-483``),
+        written as JSON lines ``log_path/histogram/<name>.jsonl`` (TensorBoard is not installed):
+        TensorBoard's bucketing in float64 -- ``bucket_count`` equal-width buckets from min to max
+        (a value at max in the last one), or one bucket ``[x - 0.5, x + 0.5]`` when every value is
+        ``x``; ``[left, right, count]`` per bucket. Computed on the weights' device."""
+        self.sync_weights()   # multi-GPU: the shards are the authoritative entity rows
+        path = os.path.join(self.log_path, "histogram")
+        os.makedirs(path, exist_ok=True)
+        for name, w in self.model_weights.items():
+            x = w.detach().reshape(-1).to(torch.float64)
+            if x.numel() == 0:
+                buckets = []
+            else:
+                lo, hi = torch.aminmax(x)
+                lo, hi = float(lo), float(hi)
+                if lo == hi:
+                    buckets = [[lo - 0.5, hi + 0.5, float(x.numel())]]
+                else:
+                    width = (hi - lo) / bucket_count
+                    idx = torch.clamp(torch.floor((x - lo) / width).to(torch.int64), max=bucket_count - 1)
+                    counts = torch.bincount(idx, minlength=bucket_count).to(torch.float64).cpu().tolist()
+                    edges = np.linspace(lo, hi, bucket_count + 1)
+                    buckets = [[float(edges[k]), float(edges[k + 1]), counts[k]] for k in range(bucket_count)]
+            with open(os.path.join(path, "%s.jsonl" % name), "a") as f:
+                f.write(json.dumps({"step": step, "buckets": buckets}) + "\n")
 
     def _save_checkpoint(self):
         """``CheckpointManager(max_to_keep=1).save()`` (``BaseModel.py:248-253``)."""

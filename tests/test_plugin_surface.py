@@ -151,6 +151,33 @@ def test_early_stopping_restores_best(tmp_path):
     assert 1 <= len(m.val_loss_history) <= 4
 
 
+def test_scalar_and_histogram_logs(tmp_path):
+    """Per-epoch loss scalars (BaseModel.py:444-468) and weight histograms
+    (BaseModel.py:162,470-483; TensorBoard bucketing: 30 equal-width buckets
+    min..max, one [x-0.5, x+0.5] bucket for a constant tensor)."""
+    train, val, md = toy()
+    m = build("TransH")
+    m.train(train_X=train, val_X=val, metadata=md, epochs=2, batch_size=4, optimizer="SGD", seed=2,
+            log_path=str(tmp_path))
+    for split in ("train", "validation"):
+        lines = open(os.path.join(str(tmp_path), "scalar", split, "loss.jsonl")).read().splitlines()
+        assert [json.loads(x)["step"] for x in lines] == [0, 1]
+    for name, w in m.model_weights.items():
+        recs = [json.loads(x) for x in open(os.path.join(str(tmp_path), "histogram", name + ".jsonl"))]
+        assert [r["step"] for r in recs] == [0, 1]
+        b = np.array(recs[-1]["buckets"])
+        x = w.detach().double().reshape(-1).numpy()
+        assert b.shape == (30, 3) and b[:, 2].sum() == x.size
+        assert b[0, 0] == x.min() and b[-1, 1] == x.max()
+        width = (x.max() - x.min()) / 30
+        ref = np.bincount(np.minimum(np.floor((x - x.min()) / width).astype(int), 29), minlength=30)
+        assert (b[:, 2] == ref).all()
+    m.model_weights["rel_emb"] = torch.full((3, 2), 0.25)
+    m._log_embeddings_histogram(7)
+    rec = [json.loads(x) for x in open(os.path.join(str(tmp_path), "histogram", "rel_emb.jsonl"))][-1]
+    assert rec == {"step": 7, "buckets": [[-0.25, 0.75, 6.0]]}
+
+
 def test_corrupt_side_assert():
     from KGE.models.translating_based.TransE import TransE
     with pytest.raises(AssertionError, match="Invalid corrupt_side"):
