@@ -325,10 +325,15 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
       const float s = score_value_fast<SK>(Rl, A.pw, &lp, A.p);
       float c = 0.f;
       switch (A.loss_kind) {
-        case KGE_LOSS_HINGE:
-          c = (A.margin + s - sp >= 0.f) ? A.inv_bk : 0.f;
+        case KGE_LOSS_HINGE: {
+          // the hinge's on/off decision is the finalise pass's (IEEE score), so
+          // a negative on the margin is active for its own row and for its
+          // positive's rows alike (the weight itself is constant)
+          float lpi;
+          const float si = score_value<SK>(Rl, A.pw, &lpi, A.p);
+          c = (A.margin + si - sp >= 0.f) ? A.inv_bk : 0.f;
           if (valid && lead) csum += c;
-          break;
+        } break;
         case KGE_LOSS_LOGISTIC: {
           const float ex = fast_exp(s - sp);
           c = ex * __builtin_amdgcn_rcpf(1.f + ex);

@@ -200,7 +200,11 @@ def score_fn(kind, p, x, y):
     if math.isinf(p):
         lp = -torch.amax(diff, dim=-1)
     else:
-        lp = -torch.pow(torch.clamp(torch.sum(torch.pow(diff, p), dim=-1), min=1e-9), 1.0 / p)
+        R = torch.clamp(torch.sum(torch.pow(diff, p), dim=-1), min=1e-9)
+        # p = 2: sqrt, the correctly rounded form of pow(R, 1/2) (a host's
+        # vectorised powf may differ by an ulp, which decides a hinge term
+        # that sits exactly on its margin in the float32 mode)
+        lp = -(torch.sqrt(R) if p == 2 else torch.pow(R, 1.0 / p))
     if kind == "lp":
         return lp
     return -torch.pow(lp, 2)

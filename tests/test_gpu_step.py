@@ -104,12 +104,13 @@ def _spec_loss(lf):
 
 
 def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, idx=torch.int64, train=True,
-             seed=11, constraint=True, typed=None, lr=0.05, opt="sgd", flags=0, k=None, pos=None):
+             seed=11, constraint=True, typed=None, lr=0.05, opt="sgd", flags=0, k=None, pos=None, W=None,
+             oracle_dtype=None, oracle_loss=None):
     from KGE import engine, optimizers
     from KGE.ns_strategy import TypedStrategy, UniformStrategy
     dev = _dev()
     rng = np.random.default_rng(seed)
-    W = _weights(model_name, E, R, d, rng, k)
+    W = _weights(model_name, E, R, d, rng, k) if W is None else W
     if pos is None:
         pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
     pos = np.asarray(pos, dtype=np.int64)
@@ -137,9 +138,11 @@ def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, id
                         sampler="typed" if typed is not None else "uniform", typed=tt)
     lim = getattr(m, "limit", None)
     ref = orc.train_step(model_name, W, pos, neg, score=_spec_score(getattr(m, "score_fn", None))
-                         if model_name not in ("DistMult", "RESCAL") else ("dot", 0.0), loss=_spec_loss(loss_fn),
+                         if model_name not in ("DistMult", "RESCAL") else ("dot", 0.0),
+                         loss=_spec_loss(loss_fn) if oracle_loss is None else oracle_loss,
                          lr=lr, constraint=constraint if model_name != "RotatE" else False, side=side, train=train,
-                         limit=lim, optimizer=opt, constraint_weight=getattr(m, "constraint_weight", 1.0))
+                         limit=lim, optimizer=opt, constraint_weight=getattr(m, "constraint_weight", 1.0),
+                         **({} if oracle_dtype is None else {"dtype": oracle_dtype}))
     got = {k: v.cpu().numpy() for k, v in m.model_weights.items()}
     return ref, got, float(step.loss_out.item()), ps.cpu().numpy(), ns.cpu().numpy(), step, neg
 
@@ -173,6 +176,33 @@ def test_transe_matrix(hiplib, si, li):
     s, l_ = _scores()[si], _losses()[li]
     ref, got, loss, ps, ns, _, _ = run_case(hiplib, "TransE", 16, 9, 4, "h+t", s, l_)
     check(ref, got, loss, ps, ns)
+
+
+@pytest.mark.parametrize("tail", [(6.0, 7.5), (5.5, 3.0), (4.0, 6.25), (7.0, 2.5), (8.0, 1.5), (3.5, 6.0)])
+def test_hinge_negative_on_the_margin(hiplib, tail):
+    """A negative exactly on the hinge margin (margin + s - s_pos == 0 in fp32):
+    the reference's clip_by_value passes the gradient on the closed interval,
+    and the step must take that one decision for the negative's own row AND
+    for its positive's rows. Positive (e0, r0, e1) with h + r - t = (-3, -4)
+    (s_pos = -5 exactly); tail e2 at a non-square distance in [5, 10] and
+    margin = fl32(sqrt(R_neg) - 5), so (margin + s) - s_pos is exactly 0
+    (Sterbenz). The oracle (float32) runs with the margin raised by 1e-5, so
+    every boundary term is active there whatever its host's sqrt rounding;
+    the hinge weight does not depend on the margin, so the updated rows must
+    agree, and the loss within its tolerance."""
+    from KGE import loss, score
+    rn = np.float32(tail[0]) ** 2 + np.float32(tail[1]) ** 2
+    margin = float(np.float32(np.sqrt(rn, dtype=np.float32) - np.float32(5.0)))
+    assert (np.float32(margin) - np.sqrt(rn, dtype=np.float32)) - np.float32(-5.0) == 0.0
+    W = {"ent_emb": np.array([[0, 0, 0, 0], [3, 4, 0, 0], [tail[0], tail[1], 0, 0]], np.float32),
+         "rel_emb": np.zeros((1, 4), np.float32)}
+    pos = np.tile(np.array([[0, 0, 1]], np.int64), (16, 1))
+    ref, got, l_, ps, ns, _, neg = run_case(hiplib, "TransE", 4, 16, 4, "t", score.LpDistance(2),
+                                            loss.PairwiseHingeLoss(margin), E=3, R=1, constraint=False, W=W,
+                                            pos=pos, oracle_dtype=torch.float32,
+                                            oracle_loss=("hinge", margin + 1e-5))
+    assert (np.asarray(neg) == 2).any()   # the boundary tail was drawn
+    check(ref, got, l_, ps, ns)
 
 
 @pytest.mark.parametrize("side", ["h", "t", "h+t"])
