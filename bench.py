@@ -65,7 +65,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-exchange", action="store_true",
-                    help="c5 at one GPU: run the all-to-all exchange + row cache instead of the one-rank shortcut")
+                    help="one GPU: run the multi-GPU step (c5: all-to-all exchange + row cache instead of the "
+                         "one-rank shortcut; other workloads: the sharded step with its exchange) as a rehearsal")
     return ap.parse_args()
 
 
@@ -285,7 +286,7 @@ def main():
         E = w["E"]
         R = w.get("R", R)
     B, K, d = w["B"], w["K"], w["d"]
-    sharded = world > 1 or w.get("sharded", False)
+    sharded = world > 1 or w.get("sharded", False) or args.force_exchange
     if sharded and world == 1:
         # one-rank process group: the same sharded step (and its exchange) as at N > 1
         import socket

@@ -1,35 +1,42 @@
-"""Multi-GPU training step: data-parallel over triples, entity tables row-sharded.
+"""Multi-GPU training step: data-parallel over triples.
 
 The reference is single-device (``BaseModel.py:19-21``); this is the build's
 one parallel strategy. One process per GPU,
 ``torch.distributed`` with the RCCL backend ("nccl" on ROCm) over xGMI.
 
-Ownership: entity row ``e`` lives on rank ``e mod G`` at local row ``e div G``
-(modulo keeps FB15k-237's degree load within 1.05x at G = 8; id blocks give
-2.24x because ``index_kg`` numbers entities in first-appearance order). The
-entity tables of a model (``ent_emb``, TransD's ``ent_proj``) share one
-``shard`` buffer, row = [ent | ent_aux]. Relation tables are replicated.
+Two exchanges, chosen by the entity table's size ("auto": dense up to 1 GiB):
 
-One step (``ShardedStep.__call__``), every rank with its own B positives:
+* ``dense`` (FB15k-237 scale, where a step touches every row anyway): every
+  rank keeps the whole table (identical replicas). A step is ``kge_step`` in
+  ``KGE_OPT_GRAD`` mode on the local batch (in-register draws from
+  rank-disjoint counter planes, loss normalised by the GLOBAL batch), then ONE
+  ``all_reduce`` of one buffer [entity gradients | relation gradients |
+  norm^2 x4 | loss], then the same clip + SGD / Adam apply on every rank
+  (ring all-reduce hands every rank the same sums, so the replicas stay
+  bit-identical). One collective per step, no gather.
+* ``sparse`` (tables > 1 GiB, C5): the entity rows are sharded, row ``e`` on
+  rank ``e mod G`` at local row ``e div G`` (modulo keeps FB15k-237's degree
+  load within 1.05x at G = 8; id blocks give 2.24x because ``index_kg``
+  numbers entities in first-appearance order). The entity tables of a model
+  (``ent_emb``, TransD's ``ent_proj``) share one ``shard`` buffer, row =
+  [ent | ent_aux]. Relation tables are replicated.
+
+One sparse step (``ShardedStep.__call__``), every rank with its own B positives:
   0. ``_constraint_loss`` assigns on the owned rows (TransE / DistMult
      renormalise, TransR / TransD clip; ``BaseModel.py:319`` order) and on the
      replicated relation tables;
   1. negatives drawn with ``kge_sample`` from rank-disjoint counter planes;
-  2. exchange the rows the batch needs into a local row cache:
-     * ``sparse`` (default for tables > 1 GiB, C5): sort + unique of the
-       batch's ids, one ``all_to_all_single`` of per-owner counts, one of the
-       ids, the owners gather their rows, one ``all_to_all_single`` of the rows
-       back -- the cache holds exactly the unique rows, in request order;
-     * ``dense`` (small tables, FB15k-237 scale where every row is touched
-       anyway): ``all_gather_into_tensor`` of the shards -- fixed sizes, no
-       host sync;
+  2. exchange the rows the batch needs into a local row cache: sort + unique
+     of the batch's ids, one ``all_to_all_single`` of per-owner counts, one of
+     the ids, the owners gather their rows, one ``all_to_all_single`` of the
+     rows back -- the cache holds exactly the unique rows, in request order;
   3. ``kge_step`` in ``KGE_OPT_GRAD`` mode on the cache (ids remapped to cache
      rows, negatives given): gather, score, loss normalised by the GLOBAL
      batch (``batch_scale = G``), duplicate-summed gradient rows of the cache,
      per-variable slice norm^2;
   4. one ``all_reduce`` of [relation gradients | norm^2 x4 | loss];
   5. the cache's gradient rows go back to their owners (``all_to_all_single``
-     with the request splits reversed / ``reduce_scatter_tensor``);
+     with the request splits reversed);
   6. owners sum each row's contributions in source-rank order (unique indices
      per source: deterministic) and apply clip_by_norm with the global norm
      + SGD on the touched rows only (``kge_apply_rows``; Adam: dense keras
@@ -52,7 +59,7 @@ from .constraint import clip_constraint, normalized_embeddings
 
 _RENORM = (_hip.MODEL_TRANSE, _hip.MODEL_DISTMULT)
 _CLIP = (_hip.MODEL_TRANSR, _hip.MODEL_TRANSD)
-DENSE_TABLE_BYTES = 1 << 30   # "auto": all-gather below this entity-table size
+DENSE_TABLE_BYTES = 1 << 30   # "auto": replicated tables + one all-reduce below this entity-table size
 
 
 class Exchange:
@@ -70,14 +77,6 @@ class Exchange:
             dist.all_gather_into_tensor(full, shard, group=self.group)
         else:
             dist.all_gather(list(full.chunk(self.world)), shard, group=self.group)
-
-    def reduce_scatter(self, shard, full):
-        if self.tensor_forms:
-            dist.reduce_scatter_tensor(shard, full, op=dist.ReduceOp.SUM, group=self.group)
-        else:
-            t = full.clone()
-            dist.all_reduce(t, group=self.group)
-            shard.copy_(t.chunk(self.world)[self.rank])
 
     def all_reduce(self, t):
         dist.all_reduce(t, group=self.group)
@@ -119,20 +118,24 @@ class ShardedStep:
         if mode not in ("dense", "sparse"):
             raise ValueError("mode must be 'auto', 'dense' or 'sparse'")
         self.mode = mode
-        # owned rows [ent | ent_aux], padded to Es rows
-        self.shard = torch.zeros(self.Es, C, dtype=torch.float32, device=dev)
-        self.shard[:self.valid, :self.ce] = ent.reshape(E, -1)[g::G]
-        if self.ca:
-            self.shard[:self.valid, self.ce:] = t["ent_aux"].reshape(E, -1)[g::G]
-        if mode == "dense":
-            self.full = torch.zeros(G * self.Es, C, dtype=torch.float32, device=dev)
-            self.gfull = [torch.zeros(G * self.Es, c, dtype=torch.float32, device=dev) for c in self._ecols()]
-            self.gshard = [torch.zeros(self.Es, c, dtype=torch.float32, device=dev) for c in self._ecols()]
-        # replicated relation tables and the all-reduce buffer
+        if mode == "sparse":
+            # owned rows [ent | ent_aux], padded to Es rows
+            self.shard = torch.zeros(self.Es, C, dtype=torch.float32, device=dev)
+            self.shard[:self.valid, :self.ce] = ent.reshape(E, -1)[g::G]
+            if self.ca:
+                self.shard[:self.valid, self.ce:] = t["ent_aux"].reshape(E, -1)[g::G]
+        # the all-reduce buffer: [entity gradients (dense mode) | relation
+        # gradients | norm^2 x4 | loss]
         self.rel_roles = [r for r in ("rel", "rel_aux") if t.get(r) is not None]
+        ent_sizes = [E * c for c in self._ecols()] if mode == "dense" else []
         sizes = [t[r].numel() for r in self.rel_roles]
-        self.red = torch.zeros(sum(sizes) + 8, dtype=torch.float32, device=dev)
-        self.grel, o = {}, 0
+        self.red = torch.zeros(sum(ent_sizes) + sum(sizes) + 8, dtype=torch.float32, device=dev)
+        o = 0
+        self.gent = []
+        for n, c in zip(ent_sizes, self._ecols()):
+            self.gent.append(self.red[o:o + n].view(E, c))
+            o += n
+        self.grel = {}
         for r, n in zip(self.rel_roles, sizes):
             self.grel[r] = self.red[o:o + n].view(t[r].shape[0], -1)
             o += n
@@ -155,8 +158,7 @@ class ShardedStep:
             f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT
             if mode == "sparse":   # every cache row [0, U) is a batch id: no gradient zero-fill
                 f.flags |= _hip.FLAG_GRAD_ROWS_TOUCHED
-            else:   # the kernels map global ids to rows of the gathered shards and draw in-register
-                f.shard = (G, self.Es, E)
+            else:   # the replica, global ids, in-register draws from rank-disjoint planes
                 f.plane_fn = lambda ns, n: ns.take_planes(n) * G + g * n
             self.fused = f
         elif engine.backend() != "eager":
@@ -174,18 +176,23 @@ class ShardedStep:
     def _ecols(self):
         return [self.ce] + ([self.ca] if self.ca else [])
 
+    def _ent_rows(self, k):
+        """Dense mode: entity table k (0 ent_emb, 1 ent_proj) as [E, cols] rows."""
+        return self.tables["ent" if k == 0 else "ent_aux"].view(self.E, -1)
+
     # ------------------------------------------------------------ phases
     def _constrain(self):
         """_constraint_loss assigns (BaseModel.py:319): owned entity rows, and
-        the replicated relation tables identically on every rank."""
-        rows = self.shard[:self.valid, :self.ce]
+        the replicated relation tables identically on every rank (dense mode:
+        the whole replica)."""
+        rows = self.shard[:self.valid, :self.ce] if self.mode == "sparse" else self._ent_rows(0)
         rel = self.tables["rel"]
         if self.fused is not None:
             st = _hip.stream_handle(self.device)
-            if self.renorm and self.valid:
+            if self.renorm and rows.shape[0]:
                 _hip.check(self.lib.kge_constrain_rows(_hip.table(rows), 0, 1.0, st), "kge_constrain_rows")
             if self.clip:
-                if self.valid:
+                if rows.shape[0]:
                     _hip.check(self.lib.kge_constrain_rows(_hip.table(rows), 1, 1.0, st), "kge_constrain_rows")
                 _hip.check(self.lib.kge_constrain_rows(_hip.table(rel), 1, 1.0, st), "kge_constrain_rows")
             if self.hyper:
@@ -193,7 +200,7 @@ class ShardedStep:
                            "kge_constrain_rows")
             return
         with torch.no_grad():
-            if self.renorm and self.valid:
+            if self.renorm and rows.shape[0]:
                 rows.copy_(normalized_embeddings(rows, p=2, value=1, axis=1))
             if self.clip:
                 rows.copy_(clip_constraint(rows, p=2, value=1, axis=-1))
@@ -273,12 +280,12 @@ class ShardedStep:
             t["ent_aux"] = cache[:, self.ce:]
         return t
 
-    def _local_grads(self, batch, neg, is_train, optimizer, cache, gbufs, prof_events=None):
-        """kge_step (KGE_OPT_GRAD) on the cache; gbufs receive the cache's
-        duplicate-summed gradient rows."""
+    def _local_grads(self, batch, neg, is_train, optimizer, lt, gbufs, prof_events=None):
+        """kge_step (KGE_OPT_GRAD) on the tables ``lt`` (the row cache, or the
+        replica); gbufs receive their duplicate-summed gradient rows."""
         if self.fused is not None:
             f = self.fused
-            f.tables = self._local_tables(cache)
+            f.tables = lt
             grads = [gbufs[0], self.grel["rel"]]
             if "rel_aux" in self.grel:
                 grads.append(self.grel["rel_aux"])
@@ -290,7 +297,6 @@ class ShardedStep:
         # host-only (KGE_BACKEND=eager) restatement of the same phase, for the gloo tests
         m = self.model
         saved = dict(m.model_weights)
-        lt = self._local_tables(cache)
         try:
             m.model_weights[self.names["ent"]] = lt["ent"]
             if self.ca:
@@ -416,57 +422,44 @@ class ShardedStep:
         if isinstance(optimizer, _opt.Adam) and is_train:
             optimizer.iterations += 1
         self._constrain()
-        if self.mode == "dense" and self.fused is not None:
-            # global ids straight into kge_step: the kernels draw the negatives
-            # and map every id to its row of the gathered table
-            self.ex.all_gather(self.full, self.shard)
-            self._local_grads(batch, neg_ids, is_train, optimizer, self.full, self.gfull, prof_events)
+        if self.mode == "dense":
+            # the replica: global ids straight into kge_step (in-kernel draws
+            # on the GPU; the host restatement takes the given negatives), then
+            # one all-reduce and the same apply on every rank
+            self._local_grads(batch, neg_ids, is_train, optimizer, dict(self.tables), self.gent, prof_events)
             self.ex.all_reduce(self.red)
             if is_train:
-                self._dense_apply(optimizer)
+                for k, gk in enumerate(self.gent):
+                    self._apply_dense(self._ent_rows(k), gk, self._slot(k), optimizer,
+                                      self.names["ent" if k == 0 else "ent_aux"])
+                self._apply_rel(optimizer)
             return self.loss
         if neg_ids is None:
             neg_ids = self._draw(batch)
         Bn = int(batch.shape[0])
         ids = torch.cat([batch[:, 0], batch[:, 2], neg_ids.to(batch.dtype)]).to(torch.int64)
-        if self.mode == "sparse":
-            self._bmax = max(getattr(self, "_bmax", 0), Bn)
-            cache, remap, plan = self._fetch_sparse(ids)
-            gbufs = self._gcache if self.fused is not None else [torch.zeros(cache.shape[0], c) for c in self._ecols()]
-        else:
-            self.ex.all_gather(self.full, self.shard)
-            cache = self.full
-            G, Es = self.G, self.Es
-            remap = (ids % G) * Es + torch.div(ids, G, rounding_mode="floor")
-            gbufs = self.gfull
+        self._bmax = max(getattr(self, "_bmax", 0), Bn)
+        cache, remap, plan = self._fetch_sparse(ids)
+        gbufs = self._gcache if self.fused is not None else [torch.zeros(cache.shape[0], c) for c in self._ecols()]
         lb = batch.clone()
         lb[:, 0] = remap[:Bn].to(batch.dtype)
         lb[:, 2] = remap[Bn:2 * Bn].to(batch.dtype)
         lneg = remap[2 * Bn:].to(batch.dtype).contiguous()
-        self._local_grads(lb, lneg, is_train, optimizer, cache, gbufs, prof_events)
+        self._local_grads(lb, lneg, is_train, optimizer, self._local_tables(cache), gbufs, prof_events)
         self.ex.all_reduce(self.red)
         if is_train:
-            if self.mode == "sparse":
-                self._apply_sparse(optimizer, gbufs, *plan)
-            else:
-                self._dense_apply(optimizer, apply_rel=False)
+            self._apply_sparse(optimizer, gbufs, *plan)
             self._apply_rel(optimizer)
         return self.loss
-
-    def _dense_apply(self, optimizer, apply_rel=True):
-        for k in range(len(self.gfull)):
-            self.ex.reduce_scatter(self.gshard[k], self.gfull[k])
-            lo = 0 if k == 0 else self.ce
-            var = self.shard[:self.valid, lo:lo + self.gfull[k].shape[1]]
-            self._apply_dense(var, self.gshard[k][:self.valid], self._slot(k), optimizer, self._shard_name(k))
-        if apply_rel:
-            self._apply_rel(optimizer)
 
     # ------------------------------------------------------------ state
     def release_entity_tables(self):
         """Drop the id-order entity tables the model held (the shards are
         authoritative; sync() allocates them again). Frees E x cols floats per
-        table on every rank -- needed when the table is most of HBM (C5)."""
+        table on every rank -- needed when the table is most of HBM (C5)).
+        Dense mode: the tables are the replica, nothing to release."""
+        if self.mode == "dense":
+            return
         w = self.model.model_weights
         for role in ("ent", "ent_aux"):
             if role in self.names and self.tables.get(role) is not None:
@@ -476,7 +469,9 @@ class ShardedStep:
 
     def sync(self):
         """Gather the shards into ``model_weights`` in id order (evaluation,
-        checkpoints)."""
+        checkpoints). Dense mode: ``model_weights`` is the replica already."""
+        if self.mode == "dense":
+            return
         G, Es = self.G, self.Es
         full = torch.zeros(G * Es, self.C, dtype=torch.float32, device=self.device)
         self.ex.all_gather(full, self.shard)
@@ -498,6 +493,12 @@ class ShardedStep:
         """Write ``weights`` (id order) into this rank's shard and the
         replicated tables (checkpoint restore)."""
         G, g = self.G, self.g
+        if self.mode == "dense":
+            with torch.no_grad():
+                for role in ["ent"] + (["ent_aux"] if self.ca else []) + self.rel_roles:
+                    self.tables[role].copy_(torch.as_tensor(weights[self.names[role]]).to(self.device)
+                                            .reshape(self.tables[role].shape))
+            return
         with torch.no_grad():
             ent = torch.as_tensor(weights[self.names["ent"]]).to(self.device).reshape(self.E, -1)
             self.shard[:self.valid, :self.ce] = ent[g::G]

@@ -276,6 +276,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   // kernel, which writes the normalised row plus this step's SGD delta
   A.fuse_norm = fuse_norm_plan;
   A.compact = compact;
+  A.zero_untouched = A.grad_mode && !compact && !rescal && !transr && !proj;
   A.gent = d->grad_out[0];
   A.grel = d->grad_out[1];
   A.grel_aux = d->grad_out[2];
@@ -607,7 +608,9 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   hipEvent_t const* ev = (hipEvent_t const*)d->prof_events;
   if (ev) (void)hipEventRecord(ev[0], st);
   const bool zero_ent = !(d->flags & KGE_FLAG_GRAD_ROWS_TOUCHED);
-  if (A.grad_mode && !P.rescal) {   // RESCAL's dense passes write every row
+  // (RESCAL's dense passes write every row; so does a non-compact update
+  // launch in grad mode, zeros for the untouched ones)
+  if (A.grad_mode && !P.rescal && (!A.zero_untouched || d->batch == 0)) {
     if (zero_ent) (void)hipMemsetAsync(d->grad_out[0], 0, (size_t)A.ent.rows * A.ent.cols * sizeof(float), st);
     (void)hipMemsetAsync(d->grad_out[1], 0, (size_t)A.rel.rows * A.rel_gcols * sizeof(float), st);
     if (P.transr) (void)hipMemsetAsync(d->grad_out[2], 0, (size_t)TA.proj.rows * TA.proj.cols * sizeof(float), st);

@@ -53,6 +53,8 @@ struct StepArgs {
   bool pw;          // LpDistancePow
   bool rel_half;    // RotatE: relation row is the phase half-row
   bool grad_mode;   // KGE_OPT_GRAD: write summed gradients, no update
+  bool zero_untouched;   // grad mode, every row visited: untouched rows get a zero gradient row
+                         // (the gradient outputs need no zero-fill)
   bool fuse_norm;   // _constraint_loss renormalisation fused into the step (SGD path)
   int64_t B;
   int32_t Keff;     // negatives per positive actually produced

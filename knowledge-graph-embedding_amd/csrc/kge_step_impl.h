@@ -1000,6 +1000,15 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
           store_rel_row<M::CPLX, VEC, NC>(row, A.rel.row_w(r), A.rel.cols);
         }
       }
+    } else if (A.zero_untouched) {
+      if (is_ent) {
+        store_row(acc, A.gent + d * (int64_t)A.ent.cols, A.ent.cols);
+      } else {
+        float z[RV * NC];
+#pragma unroll
+        for (int q = 0; q < RV * NC; ++q) z[q] = 0.f;
+        store_rel_row<M::CPLX, VEC, NC>(z, A.grel + (d - E_) * (int64_t)A.rel_gcols, A.rel.cols);
+      }
     }
   }
   if (A.dense) {

@@ -691,8 +691,9 @@ def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
 
 @pytest.mark.parametrize("model_name", ["TransE", "RotatE", "TransD", "TransR"])
 def test_gathered_shard_layout_remap(hiplib, model_name):
-    """The dense multi-GPU exchange's table layout on one GPU: the entity
-    rows laid out as G = 3 all-gathered shards (row (e mod 3) * Es + e div 3,
+    """The C-ABI's gathered-shard mapping (for callers that all-gather
+    row-sharded tables) on one GPU: the entity rows laid out
+    as G = 3 all-gathered shards (row (e mod 3) * Es + e div 3,
     padded), kge_step given shard_count / shard_rows / global_entities draws
     and maps global ids in-kernel; un-permuted rows == the oracle step."""
     from KGE import engine, loss, optimizers, score

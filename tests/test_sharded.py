@@ -1,7 +1,8 @@
 """CPU (gloo, world size 2): the multi-GPU step (KGE/sharded.py) -- e mod G
 row ownership, negatives per rank, the sparse exchange (unique ids ->
 all_to_all of ids and rows -> local row cache -> gradient rows back ->
-owner-side sum + apply) and the dense one (all-gather / reduce-scatter),
+owner-side sum + apply) and the dense one (replicated tables, one
+all-reduce of [gradients | norms | loss], the same apply on every rank),
 global-batch loss normalisation, global clip norm -- gives the
 single-device step on the concatenated batch. The local gradient phase runs
 the host restatement (KGE_BACKEND=eager); on GPUs it is kge_step."""
@@ -80,12 +81,19 @@ def _worker(rank, port, name, loss, opt, steps, mode, out):
     m = _model(name, W, loss)
     st = ShardedStep(m, mode=mode)
     assert st.valid == len(range(rank, E, 2))
+    if mode == "dense":
+        assert not hasattr(st, "shard") and len(st.gent) == (2 if name == "TransD" else 1)
     o = optimizers.SGD(0.05) if opt == "sgd" else optimizers.Adam(0.01)
     for s in range(steps):
         b = torch.tensor(pos[rank * B:(rank + 1) * B])
         n = torch.tensor(neg[rank * B * K:(rank + 1) * B * K])
         loss_v = float(st(b, True, o, neg_ids=n))
     st.sync()
+    if mode == "dense":   # every rank holds the same replica
+        for v in m.model_weights.values():
+            t = v.detach().clone()
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            assert torch.equal(t, v.detach())
     if rank == 0:
         out.put(({k: v.detach().numpy().copy() for k, v in m.model_weights.items()}, loss_v))
     dist.barrier()
