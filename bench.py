@@ -29,6 +29,7 @@ Prints ONE JSON line (rank 0).
 import argparse
 import ctypes
 import json
+import math
 import os
 import platform
 import sys
@@ -179,14 +180,33 @@ def transe_bytes(B, K, d, E):
     return step, score, update, constrain
 
 
+def transe_update_bytes(B, K, d, E, batch, fused):
+    """What KU actually moves: every row it rewrites read and
+    written once -- all E entity rows when the constraint is fused (each is
+    renormalised), else the distinct touched rows (the batch's own entities
+    plus the expected distinct uniform draws) -- plus the batch's distinct
+    relation rows; and, served from L2, one context row (snapshot / own-row
+    gradient) + coefficient + list entry per key."""
+    ents = torch.unique(torch.cat([batch[:, 0], batch[:, 2]])).numel()
+    rels = torch.unique(batch[:, 1]).numel()
+    keys = B * K + 3 * B
+    if fused:
+        ent_rows = E
+    else:
+        ent_rows = ents + (E - ents) * (1.0 - math.exp(-B * K / E))
+    rows = 8 * d * (ent_rows + rels)
+    context = 4 * d * keys + 12 * B * K + 4 * 3 * B
+    return int(rows), int(context)
+
+
 def accounting(w, B, K, d, E, R, batch):
     """Algorithmic work per step / per dominant-kernel launch."""
     m = w["model"]
     if m == "TransE":
         step, score, upd, con = transe_bytes(B, K, d, E)
-        fused = w["constraint"]
-        return {"bound": "hbm", "step": step, "kernels": {"score_kernel": score,
-                                                           "update_kernel": upd + (con if fused else 0)}}
+        rows, context = transe_update_bytes(B, K, d, E, batch, w["constraint"])
+        return {"bound": "hbm", "step": step, "kernels": {"score_kernel": score, "update_kernel": rows + context},
+                "update_split": {"rows_bytes": rows, "context_bytes": context}}
     if m == "RotatE":
         # entity rows 2d floats (8d bytes), relation rows d phases (4d bytes)
         read = B * (2 * 8 * d + 4 * d) + B * K * 8 * d + 12 * B
@@ -392,6 +412,11 @@ def main():
                 "kernels": kern}
         if "distinct_relations" in acc:
             roof["distinct_relations"] = acc["distinct_relations"]
+        if "update_split" in acc and "update_kernel" in kern:
+            ku_s = group_ms["update_kernel"] * 1e-3
+            kern["update_kernel"].update({k: v for k, v in acc["update_split"].items()})
+            kern["update_kernel"]["GBps_rows"] = round(acc["update_split"]["rows_bytes"] / ku_s / 1e9, 1)
+            kern["update_kernel"]["GBps_context_l2"] = round(acc["update_split"]["context_bytes"] / ku_s / 1e9, 1)
     else:
         dom = names[0]
         tf = acc["kernels"][dom] / (ks * 1e-3) / 1e12
