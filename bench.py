@@ -20,10 +20,13 @@ Other legs (``--workload``; one JSON line each, same schema):
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 one process per GPU, each with its own 1024-positive batch (weak scaling, the
-global batch is N*1024); the entity table is row-sharded across the ranks
+global batch is N*1024). C2's small table is replicated with one gradient
+all-reduce per step; C5's is row-sharded with the sparse exchange
 (KGE/sharded.py).
 
-Prints ONE JSON line (rank 0).
+Prints ONE JSON line (rank 0). The default C2 line at one GPU also carries
+roofline.hbm_point: the same step on a 50M-entity table, measured live
+(FB15k-237's table sits in the Infinity Cache; that one cannot).
 """
 
 import argparse
@@ -65,6 +68,8 @@ def parse():
     ap.add_argument("--dim", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-hbm-point", action="store_true",
+                    help="c2 at one GPU: skip the live C2-50M (HBM-honest) KS measurement in roofline.hbm_point")
     ap.add_argument("--force-exchange", action="store_true",
                     help="one GPU: run the multi-GPU step (c5: all-to-all exchange + row cache instead of the "
                          "one-rank shortcut; other workloads: the sharded step with its exchange) as a rehearsal")
@@ -223,6 +228,53 @@ def accounting(w, B, K, d, E, R, batch):
     flops = 2.0 * d * d * (4 * K + 8) * B
     return {"bound": "mfma", "step_flops": flops, "kernels": {"transr_kernel": flops},
             "survey_flops": 6.0 * d * d * (K + 2) * B}
+
+
+def hbm_point(args, dev, R):
+    """roofline.hbm_point: the C2 step on a 50M-entity table (SURVEY 8(d)
+    Caveat: FB15k-237's 11.6 MB table lives in the Infinity Cache, a 40 GB one
+    cannot), measured live: 30 timed steps, then 30 with HIP events on the
+    step's stream for the KS / KU split."""
+    from KGE import engine
+    w = spec("c2-50m", args)
+    E, B, K, d = w["E"], w["B"], w["K"], w["d"]
+    model, opt = build_model(w, E, R, 0, dev)
+    step = engine.FusedStep(model)
+    g = torch.Generator(device=dev).manual_seed(2000)
+    n_w, n_t = 5, 30
+    batches = torch.stack([torch.randint(0, E, (n_w + n_t, B), generator=g, device=dev),
+                           torch.randint(0, R, (n_w + n_t, B), generator=g, device=dev),
+                           torch.randint(0, E, (n_w + n_t, B), generator=g, device=dev)], -1)
+    for s_ in range(n_w):
+        step(batches[s_], True, opt)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s_ in range(n_t):
+        step(batches[n_w + s_], True, opt)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / n_t
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(n_t)]
+    for row in evs:
+        for e in row:
+            e.record()
+    torch.cuda.synchronize()
+    handles = [(ctypes.c_void_p * 4)(*[e.cuda_event for e in row]) for row in evs]
+    for s_ in range(n_t):
+        step(batches[n_w + s_], True, opt, prof_events=handles[s_])
+    torch.cuda.synchronize()
+    step.check_status()
+    ks = float(np.mean([r[1].elapsed_time(r[2]) for r in evs]))
+    ku = float(np.mean([r[2].elapsed_time(r[3]) for r in evs]))
+    acc = accounting(w, B, K, d, E, R, batches[n_w])
+    ach = acc["kernels"]["score_kernel"] / (ks * 1e-3) / 1e9
+    rows = acc["update_split"]["rows_bytes"] / (ku * 1e-3) / 1e9
+    out = {"workload": "c2-50m: " + w["desc"] % dict(B=B, K=K, d=d, E=E), "ms_per_step": round(ms, 5),
+           "kernel": "score_kernel", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 4), "score_kernel_ms": round(ks, 5), "update_kernel_ms": round(ku, 5),
+           "update_rows_GBps": round(rows, 1)}
+    del step, model, batches
+    torch.cuda.empty_cache()
+    return out
 
 
 # ---------------------------------------------------------------- CPU baseline
@@ -426,6 +478,9 @@ def main():
                 "step": {"ms_per_step": round(ms, 5), "achieved": round(acc["step_flops"] / (ms * 1e-3) / 1e12, 2)},
                 "kernels": {dom: {"ms": round(ks, 5)}, "update+apply": {"ms": round(ku, 5)},
                             "constraint": {"ms": round(k0, 5)}}}
+    if world == 1 and args.workload == "c2" and not args.force_exchange and not args.no_hbm_point \
+            and acc["bound"] == "hbm":
+        roof["hbm_point"] = hbm_point(args, dev, R)
     cpu = None
     if world == 1 and args.workload == "c2" and not args.no_cpu_baseline:
         cpu = cpu_baseline(triples, E, R, B, K, d, args.cpu_seconds)
