@@ -48,7 +48,7 @@ struct Plan {
   // dense-gradient / relation-matrix models (RESCAL)
   uint64_t o_upart, o_sorted, o_srel, o_gproj, o_rpart, o_regpart, o_gent, o_grel;
   uint64_t o_gneg, o_dm;   // TransR
-  uint64_t o_touched, o_relseg;
+  uint64_t o_leaders, o_relseg;
   uint64_t o_gnegp, o_gpos2, o_gdense[3], o_dpart;   // TransH / TransD
   bool rescal, transr, proj, td, pj_dense;
 };
@@ -312,6 +312,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.cap = (int32_t)cap;
   A.kshift = kshift;
   A.nkeyneg = (uint32_t)(B << kshift);
+  A.npos3 = (uint32_t)(3 * B);
+  A.nkeys = (uint32_t)T;
   A.snap_cols = (int32_t)entc;
   A.gcols = (int32_t)rowlen;
   A.rel_gcols = (int32_t)(rescal ? entc : relc);
@@ -335,7 +337,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.o_list = take((uint64_t)ndest * cap * 4);
   P.o_ovf = take((uint64_t)T * 8);
   P.o_upart = take((uint64_t)P.G.gridU * 4);
-  P.o_touched = take((uint64_t)(compact ? (int64_t)P.G.gridU * kUpdWaves : 1) * 8);
+  P.o_leaders = take((uint64_t)(compact ? (int64_t)P.G.gridU * kUpdWaves : 1) * 8);
   if (rescal) {
     const int64_t nct = ceil_div(d->dim, 16);
     P.o_sorted = take((uint64_t)B * 4);
@@ -525,7 +527,7 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   A.list = (uint32_t*)(ws + P.o_list);
   A.ovf = (uint64_t*)(ws + P.o_ovf);
   A.upart = (float*)(ws + P.o_upart);
-  A.touched = (uint2*)(ws + P.o_touched);
+  A.leaders = (uint2*)(ws + P.o_leaders);
   A.gpe = A.gpos;
   A.gpe_stride = 3 * A.gcols;
   A.gpe_toff = 2 * A.gcols;

@@ -37,9 +37,7 @@ struct StepCtl {
   float loss;
   uint32_t rel_ticket;     // relation-matrix gradient workgroups done (rel norm^2)
   uint32_t reg_ticket;     // regulariser-loss workgroups done
-  uint32_t ntouched;       // compact mode: destinations filed so far by the running score kernel
   float dn2[4];            // norm^2 of the dense (duplicate-summed) gradient per variable
-  uint32_t touched_len;    // compact mode: destinations for the update kernel (set by the last score workgroup)
   uint32_t pad1[3];
 };
 
@@ -83,11 +81,14 @@ struct StepArgs {
   float* upart;     // [gridU] update-kernel norm^2 partials (dense mode)
   float* gneg;      // materialised family: [B << kshift, ent.cols] negatives' entity-row gradients
   // compact update launch (tables much larger than a step's keys): the score
-  // pass appends each destination and its first key's code to `touched`, and
-  // the update kernel visits only those rows (untouched rows are not read or
-  // written)
+  // pass writes, for every key position, (destination, code) when the key
+  // is its destination's first (list position 0), else code ~0 -- no
+  // append counter; the update launch (one wave per key position) visits
+  // only those leaders' rows (untouched rows are not read or written)
   bool compact;
-  uint2* touched;
+  uint2* leaders;
+  uint32_t npos3;    // 3 B: key positions [0, 3B) are the positives' (3 i + part), then B * Keff negatives
+  uint32_t nkeys;    // B * (Keff + 3) key positions
   // multi-table update passes (TransH / TransD): the aux-table pass runs
   // first over the same destination lists and leaves the counters for the
   // main pass; scale[] slots of the pass's entity / relation variable

@@ -121,7 +121,15 @@ __device__ __forceinline__ float neg_coef(const StepArgs& A, float s, float sp, 
 // order), or to the overflow list once that list is full
 __device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_t code) {
   const uint32_t r = atomicAdd(&A.cnt[dest], 1u);
-  if (A.compact && r == 0u) A.touched[atomicAdd(&A.ctl->ntouched, 1u)] = make_uint2((uint32_t)dest, code);
+  if (A.compact) {
+    // positives' keys first (they hold the longest lists -- relation rows,
+    // skewed entities -- which then start early instead of forming the
+    // update launch's tail), then the negatives'
+    const uint32_t kpos = code < A.nkeyneg
+        ? A.npos3 + (code >> A.kshift) * (uint32_t)A.Keff + (code & ((1u << A.kshift) - 1u))
+        : 3u * ((code - A.nkeyneg) >> 2) + ((code - A.nkeyneg) & 3u);
+    A.leaders[kpos] = make_uint2((uint32_t)dest, r == 0u ? code : 0xFFFFFFFFu);
+  }
   if (r < (uint32_t)A.cap) {
     A.list[dest * A.cap + r] = code;
   } else {
@@ -624,7 +632,6 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
         // every workgroup's keys are filed: hand the overflow length to the
         // update kernel and restart the overflow list for the next step
         A.ctl->ovf_len = __hip_atomic_exchange(&A.ctl->ovf_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        A.ctl->touched_len = __hip_atomic_exchange(&A.ctl->ntouched, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else {
         A.ctl->scale[tid - 1] = -A.lr * (A.clip_norm / fmaxf(sqrtf(s), A.clip_norm));
         if (A.norm2_out) A.norm2_out[tid - 1] = s;
@@ -667,10 +674,10 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
   int64_t d;
   bool active;
   uint32_t code1 = 0xFFFFFFFFu;   // compact: the destination's first filed code
-  if (A.compact) {   // only the destinations this step touched
-    // read unconditionally (the array is padded to the grid), with the length
-    const uint2 t = A.touched[dd];
-    active = dd < (int64_t)A.ctl->touched_len;
+  if (A.compact) {   // one wave per key position: the destinations' first keys lead
+    // (read unconditionally: the array is padded to the grid)
+    const uint2 t = A.leaders[dd];
+    active = dd < (int64_t)A.nkeys && t.y != 0xFFFFFFFFu;
     d = active ? (int64_t)t.x : 0;
     code1 = t.y;
   } else {

@@ -54,16 +54,32 @@ def run(args):
     triples, E, R = z["triples"].astype(np.int64), int(z["n_entities"]), int(z["n_relations"])
     B, K, d = args.batch, args.neg, args.dim
     dev = torch.device("cuda", 0)
+    big = args.entities > 0
+    if big:   # synthetic table (the C2-50M point): no constraint, ids drawn on the device
+        E = args.entities
     model = TransE({"embedding_size": d}, K, "h+t", score_fn=score.LpDistance(p=2),
                    loss_fn=loss.SelfAdversarialNegativeSamplingLoss(margin=3, temperature=1),
-                   ns_strategy=UniformStrategy(np.arange(E), seed=12345), constraint=True)
-    model.metadata = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
-    model._model_weights_initial = None
-    model._init_embeddings(seed=12345)
-    model._to_device()
+                   ns_strategy=UniformStrategy(np.arange(E), seed=12345), constraint=not big)
+    if big:
+        gd = torch.Generator(device=dev).manual_seed(1)
+        model.metadata = {"ind2ent": range(E), "ind2rel": list(range(R))}
+        model.model_weights = {"ent_emb": (torch.rand((E, d), generator=gd, device=dev) - 0.5) * 0.2,
+                               "rel_emb": (torch.rand((R, d), generator=gd, device=dev) - 0.5) * 0.2}
+    else:
+        model.metadata = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
+        model._model_weights_initial = None
+        model._init_embeddings(seed=12345)
+        model._to_device()
     step = engine.FusedStep(model)
     opt = optimizers.SGD(learning_rate=0.01)
-    batches = torch.from_numpy(triples[np.random.default_rng(0).integers(0, len(triples), (args.steps + 5, B))]).to(dev)
+    if big:
+        gb = torch.Generator(device=dev).manual_seed(2)
+        n = args.steps + 5
+        batches = torch.stack([torch.randint(0, E, (n, B), generator=gb, device=dev),
+                               torch.randint(0, R, (n, B), generator=gb, device=dev),
+                               torch.randint(0, E, (n, B), generator=gb, device=dev)], -1)
+    else:
+        batches = torch.from_numpy(triples[np.random.default_rng(0).integers(0, len(triples), (args.steps + 5, B))]).to(dev)
     buf = (ctypes.c_ulonglong * 64)()
     for s in range(5):
         step(batches[s], True, opt)
@@ -100,6 +116,7 @@ if __name__ == "__main__":
     ap.add_argument("--neg", type=int, default=256)
     ap.add_argument("--dim", type=int, default=200)
     ap.add_argument("--score-wgs", type=int, default=0)
+    ap.add_argument("--entities", type=int, default=0, help="synthetic table of this many rows (0: FB15k-237)")
     ap.add_argument("--update-wgs", type=int, default=3686)
     a = ap.parse_args()
     build(os.environ.get("KGE_PROF_FLAGS", "").split()) if a.cmd == "build" else run(a)

@@ -1,7 +1,7 @@
 """Score-kernel tuning variants (C2 instance only, -DKGE_ONLY_ONE).
 
     python tools/variants.py build NAME -DKGE_SLOTS_PER_WAVE=128 ...   # here: KGE/_lib/libkge_var_NAME.so
-    python tools/variants.py run NAME [NAME ...]                        # on the GPU box: bench.py per variant
+    python tools/variants.py run NAME [NAME ...] [-- --workload c2-50m]  # on the GPU box: bench.py per variant
 """
 import os
 import subprocess
@@ -27,11 +27,12 @@ def build(name, defines):
     print("built", out)
 
 
-def run(names):
+def run(names, extra=()):
     import json
     for n in names:
         env = dict(os.environ, KGE_LIB=os.path.join(LIBDIR, "libkge_var_%s.so" % n))
-        out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"], env=env,
+        out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline", "--no-hbm-point"]
+                             + list(extra), env=env,
                              capture_output=True, text=True, timeout=300)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
         if not line:
@@ -46,5 +47,7 @@ def run(names):
 if __name__ == "__main__":
     if sys.argv[1] == "build":
         build(sys.argv[2], sys.argv[3:])
-    else:
-        run(sys.argv[2:])
+    else:   # run NAME [NAME ...] [-- bench.py arguments]
+        a = sys.argv[2:]
+        cut = a.index("--") if "--" in a else len(a)
+        run(a[:cut], a[cut + 1:])
