@@ -361,14 +361,10 @@ def main():
     sharded = world > 1 or w.get("sharded", False) or args.force_exchange
     if sharded and world == 1:
         # one-rank process group: the same sharded step (and its exchange) as at N > 1
-        import socket
+        import tempfile
         import torch.distributed as dist
-        s_ = socket.socket()
-        s_.bind(("127.0.0.1", 0))
-        port = s_.getsockname()[1]
-        s_.close()
-        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
-                                device_id=dev)
+        store = os.path.join(tempfile.mkdtemp(prefix="kge_pg_"), "store")   # file store: no port to race for
+        dist.init_process_group("nccl", init_method="file://" + store, rank=0, world_size=1, device_id=dev)
     model, opt = build_model(w, E, R, rank, dev)
     if sharded:
         from KGE.sharded import ShardedStep

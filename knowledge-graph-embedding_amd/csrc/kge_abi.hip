@@ -48,7 +48,8 @@ struct Plan {
   // dense-gradient / relation-matrix models (RESCAL)
   uint64_t o_upart, o_sorted, o_srel, o_gproj, o_rpart, o_regpart, o_gent, o_grel;
   uint64_t o_gneg, o_dm;   // TransR
-  uint64_t o_leaders, o_relseg;
+  uint64_t o_leaders, o_htab, o_relseg;
+  int hbits;
   uint64_t o_gnegp, o_gpos2, o_gdense[3], o_dpart;   // TransH / TransD
   bool rescal, transr, proj, td, pj_dense;
 };
@@ -247,6 +248,16 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
                               (model == KGE_MODEL_TRANSE || model == KGE_MODEL_DISTMULT) &&
                               !(d->flags & KGE_FLAG_DEBUG_UNFUSED_CONSTRAINT);
   const bool compact = !rescal && !fuse_norm_plan && ndest > 2 * T;
+  // compact: hash slots for the destination lists, >= 2 per key
+  int hbits = 1;
+  while ((1LL << hbits) < 2 * T) ++hbits;
+  if (compact) {
+    if (hbits > 31) return fail(KGE_EUNSUPPORTED, "batch x negative_ratio too large for the hashed lists");
+    if (ndest >= (int64_t)0xFFFFFFFF) return fail(KGE_EUNSUPPORTED, "more than 2^32 - 1 destination rows");
+    cap = 64;
+    if (d->flags & KGE_FLAG_DEBUG_LIST_CAP) cap = 4;
+  }
+  const int64_t nlists = compact ? (1LL << hbits) : ndest;
   const int64_t nupd = compact ? T : ndest;
   P.G.gridU = (int)ceil_div(nupd, kUpdWaves);
   P.rescal = rescal;
@@ -329,15 +340,17 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   const int nsnap = model == KGE_MODEL_ROTATE ? 3 : (transr || proj) ? 0 : 2;
   // zero-state words first: control block, per-destination counters
   P.o_ctl = take(sizeof(StepCtl));
-  P.o_cnt = take((uint64_t)ndest * 4);
+  P.o_cnt = take((uint64_t)(compact ? 1 : ndest) * 4);
+  P.o_htab = take((uint64_t)(compact ? nlists : 1) * 8);
   P.o_coef = take((uint64_t)(B << kshift) * 8);   // indexed by destination code
   P.o_snap = take((uint64_t)B * nsnap * entc * 4);
   P.o_gpos = take((uint64_t)B * 3 * rowlen * 4);
   P.o_part = take((uint64_t)((transr || proj) ? std::max<int64_t>(nWG, B) : nWG) * 8 * 4);   // one partial per positive
-  P.o_list = take((uint64_t)ndest * cap * 4);
+  P.o_list = take((uint64_t)nlists * cap * 4);
   P.o_ovf = take((uint64_t)T * 8);
   P.o_upart = take((uint64_t)P.G.gridU * 4);
-  P.o_leaders = take((uint64_t)(compact ? (int64_t)P.G.gridU * kUpdWaves : 1) * 8);
+  P.o_leaders = take((uint64_t)(compact ? (int64_t)P.G.gridU * kUpdWaves : 1) * 16);
+  P.hbits = hbits;
   if (rescal) {
     const int64_t nct = ceil_div(d->dim, 16);
     P.o_sorted = take((uint64_t)B * 4);
@@ -527,7 +540,10 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   A.list = (uint32_t*)(ws + P.o_list);
   A.ovf = (uint64_t*)(ws + P.o_ovf);
   A.upart = (float*)(ws + P.o_upart);
-  A.leaders = (uint2*)(ws + P.o_leaders);
+  A.leaders = (uint4*)(ws + P.o_leaders);
+  A.htab = (unsigned long long*)(ws + P.o_htab);
+  A.hshift = (uint32_t)(P.hbits < 32 ? 32 - P.hbits : 0);
+  A.hmask = (uint32_t)((1LL << P.hbits) - 1);
   A.gpe = A.gpos;
   A.gpe_stride = 3 * A.gcols;
   A.gpe_toff = 2 * A.gcols;

@@ -188,10 +188,14 @@ kge_status launch_step_proj(const StepArgs& A, const StepGeom& G, const PjPlan& 
     grid2 = (unsigned)G.gridU;
   } else {
     // rel_hyper only: the relation destinations come first in the full
-    // (non-compact) mapping, so a grid of R waves visits exactly them
-    B2.compact = false;
+    // (non-compact) mapping, so a grid of R waves visits exactly them;
+    // compact: their leaders are positives' keys, the first 3B positions
     B2.rel_only = true;
-    grid2 = (unsigned)((A.rel.rows + kUpdWaves - 1) / kUpdWaves);
+    if (A.compact) {
+      grid2 = (unsigned)((A.npos3 + kUpdWaves - 1) / kUpdWaves);
+    } else {
+      grid2 = (unsigned)((A.rel.rows + kUpdWaves - 1) / kUpdWaves);
+    }
   }
   launch_update_mat_pj(B2, G.vec, G.nc, grid2, st);
   dbg_sync(st, "pass B");

@@ -86,7 +86,15 @@ struct StepArgs {
   // append counter; the update launch (one wave per key position) visits
   // only those leaders' rows (untouched rows are not read or written)
   bool compact;
-  uint2* leaders;
+  uint4* leaders;   // per key position: (destination, code or ~0, hash slot, 0)
+  // compact launches key the destination lists by a hash slot instead of the
+  // destination row (the E-sized counter / list arrays of a 50M-row table
+  // would sit in HBM; the 2T-slot table stays in L2 / MALL): per slot
+  // (destination + 1) << 32 | count, 0 = empty, linear probing; the lists
+  // are [slot, cap], the leader's update wave empties its slot
+  unsigned long long* htab;
+  uint32_t hshift;  // slot = (dest * 2654435761) >> hshift (32 - log2 slots)
+  uint32_t hmask;
   uint32_t npos3;    // 3 B: key positions [0, 3B) are the positives' (3 i + part), then B * Keff negatives
   uint32_t nkeys;    // B * (Keff + 3) key positions
   // multi-table update passes (TransH / TransD): the aux-table pass runs
@@ -115,8 +123,8 @@ struct StepArgs {
   float* snap;      // [B, NSNAP, snap_cols] positive contexts
   float* gpos;      // [B, 3, gcols] positive h / r / t row gradients
   float* part;      // [nWG, 8] loss, norm^2 x4 partials
-  uint32_t* cnt;    // [E + R] entries per destination (zero between steps)
-  uint32_t* list;   // [E + R, cap] codes per destination (arrival order)
+  uint32_t* cnt;    // [E + R] entries per destination (zero between steps; not compact)
+  uint32_t* list;   // [E + R, cap] codes per destination (arrival order; compact: [slots, cap])
   uint64_t* ovf;    // [B * (Keff + 3)] dest << 32 | code past a full list
   // KGE_OPT_GRAD outputs: dense [E, ent.cols] / [R, rel_gcols]
   float* gent;

@@ -118,20 +118,36 @@ __device__ __forceinline__ float neg_coef(const StepArgs& A, float s, float sp, 
 }
 
 // one destination key: append its code to the destination's list (arrival
-// order), or to the overflow list once that list is full
+// order), or to the overflow list once that list is full. Compact launches:
+// the list is the destination's hash slot's (one 64-bit CAS claims an empty
+// slot -- the common case on a large table -- else one atomic add on the
+// slot that holds the destination), and the key's position in the leader
+// table records (destination, code if it took list position 0, slot);
+// positives' keys first (they hold the longest lists -- relation rows,
+// skewed entities -- which then start early instead of forming the update
+// launch's tail), then the negatives'
 __device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_t code) {
-  const uint32_t r = atomicAdd(&A.cnt[dest], 1u);
+  uint32_t r;
+  int64_t li = dest;   // list index
   if (A.compact) {
-    // positives' keys first (they hold the longest lists -- relation rows,
-    // skewed entities -- which then start early instead of forming the
-    // update launch's tail), then the negatives'
+    const unsigned long long key = (unsigned long long)((uint32_t)dest + 1u) << 32;
+    uint32_t h = ((uint32_t)dest * 2654435761u) >> A.hshift;
+    for (;;) {   // at most one pass: the table has >= 2x as many slots as keys
+      const unsigned long long cur = atomicCAS(&A.htab[h], 0ull, key | 1ull);
+      if (cur == 0ull) { r = 0u; break; }
+      if ((cur & 0xFFFFFFFF00000000ull) == key) { r = (uint32_t)atomicAdd(&A.htab[h], 1ull); break; }
+      h = (h + 1u) & A.hmask;
+    }
+    li = h;
     const uint32_t kpos = code < A.nkeyneg
         ? A.npos3 + (code >> A.kshift) * (uint32_t)A.Keff + (code & ((1u << A.kshift) - 1u))
         : 3u * ((code - A.nkeyneg) >> 2) + ((code - A.nkeyneg) & 3u);
-    A.leaders[kpos] = make_uint2((uint32_t)dest, r == 0u ? code : 0xFFFFFFFFu);
+    A.leaders[kpos] = make_uint4((uint32_t)dest, r == 0u ? code : 0xFFFFFFFFu, h, 0u);
+  } else {
+    r = atomicAdd(&A.cnt[dest], 1u);
   }
   if (r < (uint32_t)A.cap) {
-    A.list[dest * A.cap + r] = code;
+    A.list[li * A.cap + r] = code;
   } else {
     const uint32_t o = atomicAdd(&A.ctl->ovf_count, 1u);
     A.ovf[o] = ((uint64_t)dest << 32) | code;
@@ -671,18 +687,20 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
   const int64_t R_ = A.rel_dests ? A.rel.rows : 0;
   const int64_t ndest = E_ + R_;
   const int64_t dd = (int64_t)blockIdx.x * kUpdWaves + wv;
-  int64_t d;
+  int64_t d, li;   // destination row, its list index (the row, or its hash slot)
   bool active;
   uint32_t code1 = 0xFFFFFFFFu;   // compact: the destination's first filed code
   if (A.compact) {   // one wave per key position: the destinations' first keys lead
     // (read unconditionally: the array is padded to the grid)
-    const uint2 t = A.leaders[dd];
-    active = dd < (int64_t)A.nkeys && t.y != 0xFFFFFFFFu;
+    const uint4 t = A.leaders[dd];
+    active = dd < (int64_t)A.nkeys && t.y != 0xFFFFFFFFu && !(A.rel_only && (int64_t)t.x < E_);
     d = active ? (int64_t)t.x : 0;
+    li = active ? (int64_t)t.z : 0;
     code1 = t.y;
   } else {
     active = dd < (A.rel_only ? R_ : ndest);
     d = dd < R_ ? E_ + dd : dd - R_;
+    li = d;
   }
   const uint32_t nneg = A.nkeyneg;
   const uint32_t kmask = (1u << A.kshift) - 1u;
@@ -772,10 +790,10 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
   float dn2 = 0.f;   // dense mode: this wave's ||summed row gradient||^2
   if (active) {
     const bool is_ent = d < E_;
-    const uint32_t* lst = A.list + d * (int64_t)A.cap;
+    const uint32_t* lst = A.list + li * (int64_t)A.cap;
     // issued together: the counter, the list's first 64 entries (speculative;
     // lanes past the count are ignored) and the entity row
-    const uint32_t n = A.cnt[d];
+    const uint32_t n = A.compact ? (uint32_t)A.htab[li] : A.cnt[d];
     const uint32_t code0 = lst[min(lane, A.cap - 1)];
     F E, acc;
     acc.zero();
@@ -807,7 +825,10 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
       }
     }
     if (n != 0u || (A.dense && is_ent)) {
-      if (lane == 0 && n != 0u && !A.keep_cnt) A.cnt[d] = 0u;   // ready for the next step
+      if (lane == 0 && n != 0u && !A.keep_cnt) {   // ready for the next step
+        if (A.compact) A.htab[li] = 0ull;
+        else A.cnt[d] = 0u;
+      }
       float racc[RV * NC];
 #pragma unroll
       for (int q = 0; q < RV * NC; ++q) racc[q] = 0.f;

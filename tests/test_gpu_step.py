@@ -7,6 +7,7 @@ updated tables |got - ref| <= 1e-5 elementwise.
 """
 
 import math
+import os
 
 import numpy as np
 import pytest
@@ -101,6 +102,13 @@ def _spec_loss(lf):
     if t is loss.SelfAdversarialNegativeSamplingLoss:
         return ("sans", lf.margin, lf.temperature)
     return ("sqerr",)
+
+
+def _init_world1(dist, dev):
+    """One-rank RCCL process group through a file store (no TCP port to race for)."""
+    import tempfile
+    path = os.path.join(tempfile.mkdtemp(prefix="kge_pg_"), "store")
+    dist.init_process_group("nccl", init_method="file://" + path, rank=0, world_size=1, device_id=dev)
 
 
 def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, idx=torch.int64, train=True,
@@ -641,18 +649,12 @@ def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
     cache -> gradient rows back -> kge_apply_rows) or dense (all-gather /
     reduce-scatter) exchange, grad-mode kge_step on the cache, all-reduce,
     two steps == two oracle steps with the same draws."""
-    import socket
     import torch.distributed as dist
     from KGE import loss, optimizers, score
     from KGE.ns_strategy import UniformStrategy
     from KGE.sharded import ShardedStep
     dev = _dev()
-    s_ = socket.socket()
-    s_.bind(("127.0.0.1", 0))
-    port = s_.getsockname()[1]
-    s_.close()
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
-                            device_id=dev)
+    _init_world1(dist, dev)
     try:
         rng = np.random.default_rng(3)
         E, R, d, B, K = 37, 5, 24, 16, 8
@@ -738,18 +740,12 @@ def test_sharded_step_c5_shard_size(hiplib):
     h+t, SANS) through the sparse exchange: finite loss, only touched rows
     change, and the owner update equals the fused single-device step on the
     same rows (same draws)."""
-    import socket
     import torch.distributed as dist
     from KGE import engine, loss, optimizers, score
     from KGE.ns_strategy import UniformStrategy
     from KGE.sharded import ShardedStep
     dev = _dev()
-    s_ = socket.socket()
-    s_.bind(("127.0.0.1", 0))
-    port = s_.getsockname()[1]
-    s_.close()
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % port, rank=0, world_size=1,
-                            device_id=dev)
+    _init_world1(dist, dev)
     try:
         E, R, d, B, K = 6_250_000, 1000, 512, 256, 256
         g = torch.Generator(device=dev).manual_seed(0)
