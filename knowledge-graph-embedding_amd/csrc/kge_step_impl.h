@@ -669,8 +669,14 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
 // score kernel) and the SGD update (BaseModel.py:328, keras SGD
 // ResourceScatterAdd) with ONE read-modify-write per touched row. The
 // destination's counter is cleared for the next step as it is read.
-template <template <int, int, int> class Model, int VEC, int NC, int SK>
-__global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
+// UW: amdgpu_waves_per_eu. The compact launch (one short wave per key over a
+// table far larger than L2) runs an 8-waves-per-SIMD instance: its latency
+// chain wants occupancy more than it minds 16 spilled registers in the
+// long-list paths (C2-50M KU 189 -> 172 us); the full launch keeps the
+// allocator's choice (71 registers, 7 waves), 2 % faster at C2.
+template <template <int, int, int> class Model, int VEC, int NC, int SK, int UW = 1>
+__global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(UW)))
+void update_kernel(StepArgs A) {
   using M = Model<VEC, NC, SK>;
   using F = Frag<VEC, NC>;
   constexpr int U = KGE_UPDATE_U / NC > 1 ? KGE_UPDATE_U / NC : 2;   // entries in flight per wave
@@ -1042,8 +1048,11 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
   if (A.dense) {
     // ||dense gradient||^2: workgroup partial, the last workgroup reduces
     // every partial in a fixed order (clip_by_norm of the dense tensor)
-    __shared__ float s_n2[kUpdWaves];
-    __shared__ int s_lastu;
+    // (in the sort scratch: 20 bytes of their own would cost a workgroup of
+    // occupancy -- 7 instead of 8 per CU at 20,480 bytes of LDS each)
+    float* s_n2 = reinterpret_cast<float*>(&s_scr[0][0]);
+    int* s_lastu = reinterpret_cast<int*>(&s_scr[0][kUpdWaves]);
+    __syncthreads();   // every wave is done with its scratch
     dn2 = wave_sum(dn2);
     if (lane == 0) s_n2[wv] = dn2;
     __syncthreads();
@@ -1053,10 +1062,10 @@ __global__ __launch_bounds__(kUpdThreads) void update_kernel(StepArgs A) {
       __hip_atomic_store(&A.upart[blockIdx.x], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_s_waitcnt(0);
       const uint32_t prev = __hip_atomic_fetch_add(&A.ctl->upd_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_lastu = prev == gridDim.x - 1;
+      *s_lastu = prev == gridDim.x - 1;
     }
     __syncthreads();
-    if (s_lastu) {
+    if (*s_lastu) {
       float acc2 = 0.f;
       for (int w = threadIdx.x; w < (int)gridDim.x; w += blockDim.x)
         acc2 += __hip_atomic_load(&A.upart[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1098,8 +1107,15 @@ template <template <int, int, int> class Model, int VEC, int NC, int SK>
 static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_t st, hipEvent_t const* ev) {
   launch_score<Model, VEC, NC, SK>(A, G, st);
   if (ev) (void)hipEventRecord(ev[2], st);
-  if (A.train)
+  if (A.train) {
+    if constexpr (NC == 1 && !Model<VEC, NC, SK>::WIDE) {
+      if (A.compact) {
+        hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK, 8>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
+        return KGE_OK;
+      }
+    }
     hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
+  }
   return KGE_OK;
 }
 
