@@ -106,9 +106,15 @@ enum {
                                        update kernel's overflow path runs */
   KGE_FLAG_DEBUG_UNFUSED_CONSTRAINT = 4, /* test hook: run the full-table renormalisation
                                        as its own kernel even on the SGD path */
-  KGE_FLAG_GRAD_ROWS_TOUCHED = 8     /* KGE_OPT_GRAD: the caller needs only the entity
+  KGE_FLAG_GRAD_ROWS_TOUCHED = 8,    /* KGE_OPT_GRAD: the caller needs only the entity
                                        gradient rows the batch touches (a row cache of
                                        exactly the batch's ids): no zero-fill of grad_out[0/3] */
+  KGE_FLAG_GRAD_RENORM = 16          /* KGE_OPT_GRAD, TransE / DistMult with constraint:
+                                       the renormalisation assign runs inside the step as on
+                                       the SGD path (rows scored normalised in registers) and
+                                       the step writes every entity row back normalised; the
+                                       caller applies its update to those rows (no full-table
+                                       pass of its own) */
 };
 
 typedef struct kge_table {

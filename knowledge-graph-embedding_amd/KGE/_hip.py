@@ -22,6 +22,7 @@ SAMPLER_UNIFORM, SAMPLER_TYPED, SAMPLER_GIVEN = range(3)
 OPT_NONE, OPT_SGD, OPT_GRAD, OPT_ADAM = range(4)
 FLAG_NO_TABLE_CONSTRAINT = 1
 FLAG_GRAD_ROWS_TOUCHED = 8
+FLAG_GRAD_RENORM = 16
 RANK_TRANS, RANK_ROT, RANK_MUL, RANK_DOT = range(4)
 RPROJ_NONE, RPROJ_HYPER, RPROJ_RANK1 = range(3)
 

@@ -160,6 +160,8 @@ class ShardedStep:
                 f.flags |= _hip.FLAG_GRAD_ROWS_TOUCHED
             else:   # the replica, global ids, in-register draws from rank-disjoint planes
                 f.plane_fn = lambda ns, n: ns.take_planes(n) * G + g * n
+                if self.renorm:   # the renormalisation assign inside the step (no K0 pass)
+                    f.flags = _hip.FLAG_GRAD_RENORM
             self.fused = f
         elif engine.backend() != "eager":
             raise RuntimeError("ShardedStep needs GPUs (or KGE_BACKEND=eager for host-only tests)")
@@ -189,7 +191,8 @@ class ShardedStep:
         rel = self.tables["rel"]
         if self.fused is not None:
             st = _hip.stream_handle(self.device)
-            if self.renorm and rows.shape[0]:
+            # (dense mode: kge_step renormalises the replica itself, KGE_FLAG_GRAD_RENORM)
+            if self.renorm and rows.shape[0] and self.mode == "sparse":
                 _hip.check(self.lib.kge_constrain_rows(_hip.table(rows), 0, 1.0, st), "kge_constrain_rows")
             if self.clip:
                 if rows.shape[0]:

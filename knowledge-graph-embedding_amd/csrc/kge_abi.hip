@@ -243,7 +243,9 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   // compact update launch: when the tables have far more rows than the step
   // has keys, visit only the touched destinations (not with a fused full-table
   // constraint or a dense gradient, which rewrite every row)
-  const bool fuse_norm_plan = d->optimizer == KGE_OPT_SGD && d->constraint &&
+  const bool fuse_norm_plan = (d->optimizer == KGE_OPT_SGD ||
+                               (d->optimizer == KGE_OPT_GRAD && (d->flags & KGE_FLAG_GRAD_RENORM))) &&
+                              d->constraint &&
                               !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT) &&
                               (model == KGE_MODEL_TRANSE || model == KGE_MODEL_DISTMULT) &&
                               !(d->flags & KGE_FLAG_DEBUG_UNFUSED_CONSTRAINT);

@@ -827,7 +827,8 @@ void update_kernel(StepArgs A) {
       load_row(E, A.ent.row(d), A.ent.cols);
       if (A.fuse_norm) {
         normalize_row(E);   // the step's constraint assign, then this step's update
-        if (n == 0u) store_row(E, A.ent.row_w(d), A.ent.cols);
+        // (grad mode: every row goes back normalised; the caller's apply follows)
+        if (n == 0u || A.grad_mode) store_row(E, A.ent.row_w(d), A.ent.cols);
       }
     }
     if (n != 0u || (A.dense && is_ent)) {
