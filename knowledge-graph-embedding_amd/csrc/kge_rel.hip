@@ -255,21 +255,55 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
 
 // ------------------------------------------------------------ KL regulariser loss
 // lambda * (sum_e ||e||^2 / E + sum_r ||R_r||_F^2 / R): per-workgroup
-// partials, the last workgroup adds the term to the step loss.
+// partials, the last workgroup adds the term to the step loss. Balanced
+// sweep: the unit of work is a 256-float chunk of a row (a float4 per lane),
+// so the R relation matrices (d^2 floats each) spread over every wave instead
+// of one wave per matrix; units are dealt to waves in a fixed order
+// (deterministic sums).
+__device__ __forceinline__ float chunk_sq(const float* x, int64_t c0, int cols, int lane, bool a16) {
+  const int64_t c = c0 + 4 * lane;
+  float s = 0.f;
+  if (a16 && c + 3 < cols) {
+    const float4 v = *reinterpret_cast<const float4*>(x + c);
+    s = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  } else {
+    for (int64_t k = c; k < c0 + 4 * lane + 4 && k < cols; ++k) s += x[k] * x[k];
+  }
+  return s;
+}
+
 __global__ __launch_bounds__(256) void reg_loss_kernel(TabView ent, TabView rel, float lam, float* part,
                                                         StepCtl* ctl, float* loss_out, float* loss_accum) {
   __shared__ float s_p[4][2];
   __shared__ int s_last;
   const int lane = lane_id(), wv = wave_id();
   const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t upe = (ent.cols + 255) / 256, upr = (rel.cols + 255) / 256;   // chunks per row
+  const int64_t ue = ent.rows * upe, ur = rel.rows * upr;
+  const bool ae = ((uintptr_t)ent.p % 16 == 0) && ent.ld % 4 == 0;
+  const bool ar = ((uintptr_t)rel.p % 16 == 0) && rel.ld % 4 == 0;
   float se = 0.f, sr = 0.f;
-  for (int64_t row = (int64_t)blockIdx.x * 4 + wv; row < ent.rows + rel.rows; row += nw) {
-    const bool is_e = row < ent.rows;
-    const float* x = is_e ? ent.row(row) : rel.row(row - ent.rows);
-    const int cols = is_e ? ent.cols : rel.cols;
-    float s = 0.f;
-    for (int c = lane; c < cols; c += KGE_WAVE) s += x[c] * x[c];
-    if (is_e) se += s; else sr += s;
+  // four units in flight per wave (their loads issued before any is summed)
+  for (int64_t u0 = (int64_t)blockIdx.x * 4 + wv; u0 < ue + ur; u0 += 4 * nw) {
+    float q[4];
+    bool isr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t u = u0 + k * nw;
+      q[k] = 0.f;
+      isr[k] = u >= ue;
+      if (u < ue) {
+        const int64_t row = u / upe;
+        q[k] = chunk_sq(ent.row(row), (u - row * upe) * 256, ent.cols, lane, ae);
+      } else if (u < ue + ur) {
+        const int64_t v = u - ue, row = v / upr;
+        q[k] = chunk_sq(rel.row(row), (v - row * upr) * 256, rel.cols, lane, ar);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (isr[k]) sr += q[k]; else se += q[k];
+    }
   }
   se = wave_sum(se);
   sr = wave_sum(sr);

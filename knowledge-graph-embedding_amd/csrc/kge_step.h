@@ -181,7 +181,7 @@ void launch_rel_post(const RelArgs& R, hipStream_t st);     // g_h, g_t, dR (+ d
 // lambda * (mean_e ||e||^2 + mean_r ||R_r||_F^2) added to the step loss (RESCAL.py:190-198)
 void launch_reg_loss(const TabView& ent, const TabView& rel, float lam, float* part, StepCtl* ctl,
                      float* loss_out, float* loss_accum, hipStream_t st);
-constexpr int kRegWGs = 256;
+constexpr int kRegWGs = 1024;   // regulariser sweep workgroups (256-float chunks dealt round-robin)
 
 // first sorted position in [lo, hi) whose relation is >= r (srel ascending)
 __device__ __forceinline__ int64_t rel_lower(const int32_t* srel, int64_t lo, int64_t hi, int64_t r) {
