@@ -1,6 +1,7 @@
 """Misc helpers (reference ``KGE/utils.py:6-25``)."""
 
 import os
+import shutil
 import stat
 
 import numpy as np
@@ -26,12 +27,9 @@ def ns_with_same_type(x, metadata, negative_ratio):
 
 
 def rmtree(top):
-    """Remove a directory tree, forcing write permission (``utils.py:18-25``)."""
-    for root, dirs, files in os.walk(top, topdown=False):
-        for name in files:
-            filename = os.path.join(root, name)
-            os.chmod(filename, stat.S_IWUSR)
-            os.remove(filename)
-        for name in dirs:
-            os.rmdir(os.path.join(root, name))
-    os.rmdir(top)
+    """Remove a directory tree even where files are read-only (``utils.py:18-25``):
+    a failed unlink gets write permission and is retried once."""
+    def _retry(func, path, _exc):
+        os.chmod(path, stat.S_IWUSR | stat.S_IRUSR | stat.S_IXUSR)
+        func(path)
+    shutil.rmtree(top, onerror=_retry)
