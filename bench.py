@@ -272,6 +272,9 @@ def hbm_point(args, dev, R):
            "kernel": "score_kernel", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(ach / HBM_PEAK_GBS, 4), "score_kernel_ms": round(ks, 5), "update_kernel_ms": round(ku, 5),
            "update_rows_GBps": round(rows, 1)}
+    pmc = pmc_traffic("c2-50m")
+    out["traffic"] = pmc["kernels"]["score_kernel"].get("hbm_bytes_per_launch") \
+        if pmc and "score_kernel" in pmc.get("kernels", {}) else None
     del step, model, batches
     torch.cuda.empty_cache()
     return out

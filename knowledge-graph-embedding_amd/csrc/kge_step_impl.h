@@ -33,6 +33,9 @@
 
 #include "kge_step.h"
 
+#ifndef KGE_SCORE_PREFETCH
+#define KGE_SCORE_PREFETCH 0   // score kernel: software-pipelined row batches (tuning knob)
+#endif
 #ifndef KGE_STREAM_ROWS
 #define KGE_STREAM_ROWS 8   // sampled rows per stream batch at NC = 1 (tuning knob)
 #endif
@@ -300,21 +303,35 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
     constexpr bool RAW = M::NRM_FROM_R && NC == 1;
     const bool lane_in = lane * VEC < A.ent.cols;
     int idv = 0;   // the wave's next 64 slot ids, one per lane
-    for (int j0 = jbeg; j0 < jend; j0 += ROWS) {
-      if (((j0 - jbeg) & (KGE_WAVE - 1)) == 0) idv = (j0 + lane < jend) ? ids[j0 + lane] : 0;
-      const int jo = (j0 - jbeg) & (KGE_WAVE - 1);
-      const int nrow = min(ROWS, jend - j0);   // wave-uniform, >= 1
-      // every row's load is issued before any is used; rows past the slot
-      // range repeat the last valid row (finite values, weight 0)
-      // (NRM_FROM_R models: lanes past the row's end keep whatever they
-      // loaded and only their score partial is masked -- their accumulator
-      // lanes are never read back)
-      F E[ROWS];
+    // every row's load is issued before any is used; rows past the slot
+    // range repeat the last valid row (finite values, weight 0)
+    // (NRM_FROM_R models: lanes past the row's end keep whatever they
+    // loaded and only their score partial is masked -- their accumulator
+    // lanes are never read back)
+    auto issue = [&](F (&dst)[ROWS], int jb) {
+      if (((jb - jbeg) & (KGE_WAVE - 1)) == 0) idv = (jb + lane < jend) ? ids[jb + lane] : 0;
+      const int jo = (jb - jbeg) & (KGE_WAVE - 1);
+      const int nr = min(ROWS, jend - jb);
 #pragma unroll
       for (int u = 0; u < ROWS; ++u) {
-        const float* row = A.ent.row(__builtin_amdgcn_readlane(idv, jo + min(u, nrow - 1)));
-        if (RAW) load_row_raw(E[u], row, A.ent.cols);
-        else load_row(E[u], row, A.ent.cols);
+        const float* row = A.ent.row(__builtin_amdgcn_readlane(idv, jo + min(u, nr - 1)));
+        if (RAW) load_row_raw(dst[u], row, A.ent.cols);
+        else load_row(dst[u], row, A.ent.cols);
+      }
+    };
+    // KGE_SCORE_PREFETCH: the next batch's rows are in flight while this
+    // batch is reduced and differentiated (one more batch of registers)
+    F En[KGE_SCORE_PREFETCH ? ROWS : 1];
+    if constexpr (KGE_SCORE_PREFETCH) issue(En, jbeg);
+    for (int j0 = jbeg; j0 < jend; j0 += ROWS) {
+      const int nrow = min(ROWS, jend - j0);   // wave-uniform, >= 1
+      F E[ROWS];
+      if constexpr (KGE_SCORE_PREFETCH) {
+#pragma unroll
+        for (int u = 0; u < ROWS; ++u) E[u] = En[u];
+        if (j0 + ROWS < jend) issue(En, j0 + ROWS);
+      } else {
+        issue(E, j0);
       }
       if (A.fuse_norm) {
         // fused _constraint_loss: each sampled row normalised in registers

@@ -11,7 +11,7 @@ for w in $LEGS; do
   timeout -k 10 300 python -u bench.py --workload $w --no-cpu-baseline > "$OUT/bench_$w.json" 2> "$OUT/bench_$w.err" || { echo "bench $w failed"; tail -20 "$OUT/bench_$w.err"; exit 3; }
   cat "$OUT/bench_$w.json"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$w" -o run --output-format csv -- \
-    python3 bench.py --workload $w --steps 50 --warmup 5 --no-cpu-baseline > /dev/null 2> "$OUT/prof_$w.err" || { echo "rocprof $w failed"; tail -20 "$OUT/prof_$w.err"; exit 4; }
+    python3 bench.py --workload $w --steps 50 --warmup 5 --no-cpu-baseline --no-hbm-point > /dev/null 2> "$OUT/prof_$w.err" || { echo "rocprof $w failed"; tail -20 "$OUT/prof_$w.err"; exit 4; }
   find "$OUT/prof_$w" -name "*kernel_stats.csv" -exec cat {} \; | cut -d, -f1-8 | head -14
 done
 echo ALL_OK
