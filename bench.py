@@ -46,8 +46,13 @@ for p in (ROOT, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-# RCCL's version banner goes to stdout; the contract is ONE JSON line there
+# The contract is ONE JSON line on stdout, but RCCL prints its banner and
+# warnings (e.g. the iommu=pt notice) there: the process's fd 1 goes to stderr
+# for the whole run and only the result line is written to the real stdout.
 os.environ["NCCL_DEBUG"] = "WARN"
+_RESULT_OUT = os.fdopen(os.dup(1), "w")
+sys.stdout.flush()
+os.dup2(2, 1)
 
 import torch  # noqa: E402
 
@@ -501,7 +506,8 @@ def main():
     if sharded:
         out["config"]["exchange"] = "local (one rank: fused step on the shard)" if step.direct is not None \
             else step.mode
-    print(json.dumps(out))
+    _RESULT_OUT.write(json.dumps(out) + "\n")
+    _RESULT_OUT.flush()
     if sharded:
         torch.distributed.destroy_process_group()
 

@@ -1,6 +1,7 @@
 """Score-kernel tuning variants (C2 instance only, -DKGE_ONLY_ONE).
 
     python tools/variants.py build NAME -DKGE_SLOTS_PER_WAVE=128 ...   # here: KGE/_lib/libkge_var_NAME.so
+    python tools/variants.py buildfull NAME -D...   # every model family (all library sources)
     python tools/variants.py run NAME [NAME ...] [-- --workload c2-50m]  # on the GPU box: bench.py per variant
 """
 import os
@@ -12,11 +13,18 @@ CSRC = os.path.join(ROOT, "knowledge-graph-embedding_amd", "csrc")
 LIBDIR = os.path.join(ROOT, "knowledge-graph-embedding_amd", "KGE", "_lib")
 
 
-def build(name, defines):
+def build(name, defines, full=False):
     objs, procs = [], []
-    for src in ("kge_step.hip", "kge_abi.hip", "kge_transr.hip", "kge_rel.hip", "kge_stream.hip"):
+    if full:
+        sys.path.insert(0, ROOT)
+        import __graft_entry__
+        sources, defines = __graft_entry__.SOURCES, list(defines)
+    else:
+        sources, defines = ("kge_step.hip", "kge_abi.hip", "kge_transr.hip", "kge_rel.hip", "kge_stream.hip"), \
+            ["-DKGE_ONLY_ONE"] + list(defines)
+    for src in sources:
         obj = "/tmp/var_%s_%s" % (name, src.replace(".hip", ".o"))
-        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DKGE_ONLY_ONE"] + defines + \
+        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"] + defines + \
               ["-c", os.path.join(CSRC, src), "-o", obj]
         procs.append(subprocess.Popen(cmd))
         objs.append(obj)
@@ -45,8 +53,8 @@ def run(names, extra=()):
 
 
 if __name__ == "__main__":
-    if sys.argv[1] == "build":
-        build(sys.argv[2], sys.argv[3:])
+    if sys.argv[1] in ("build", "buildfull"):
+        build(sys.argv[2], sys.argv[3:], full=sys.argv[1] == "buildfull")
     else:   # run NAME [NAME ...] [-- bench.py arguments]
         a = sys.argv[2:]
         cut = a.index("--") if "--" in a else len(a)
