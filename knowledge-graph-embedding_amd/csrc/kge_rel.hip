@@ -78,6 +78,48 @@ __global__ __launch_bounds__(256) void rel_rank_kernel(RelArgs P) {
   }
 }
 
+// Small batches: a wave per item (positive t and relation t), its lanes
+// sweeping the batch's relation ids straight from the triples (L2 hits after
+// the first wave) and summing the four counts with integer butterflies --
+// B / 64 loads per lane instead of a B-long serial loop per thread in two
+// workgroups. Same counts, so the same stable order.
+__device__ __forceinline__ int wave_isum(int x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, KGE_WAVE);
+  return x;
+}
+__global__ __launch_bounds__(256) void rel_rank_wave_kernel(RelArgs P) {
+  const int lane = lane_id();
+  const int64_t t = (int64_t)blockIdx.x * 4 + wave_id();
+  const bool doi = t < P.B, dor = t < P.rel.rows;
+  if (!doi && !dor) return;
+  const int32_t ri = doi ? (int32_t)pos_id(P, t, 1) : -1;
+  const int32_t rr = (int32_t)t;
+  int lt = 0, eq = 0, rlt = 0, rcnt = 0;
+#pragma unroll 8
+  for (int64_t j = lane; j < P.B; j += KGE_WAVE) {
+    const int32_t x = (int32_t)pos_id(P, j, 1);
+    lt += x < ri;
+    eq += x == ri && j < t;
+    rlt += x < rr;
+    rcnt += x == rr;
+  }
+  lt = wave_isum(lt);
+  eq = wave_isum(eq);
+  rlt = wave_isum(rlt);
+  rcnt = wave_isum(rcnt);
+  if (lane == 0) {
+    if (doi) {
+      P.sorted[lt + eq] = (int32_t)t;
+      P.srel[lt + eq] = ri;
+    }
+    if (dor) {
+      P.rel_beg[t] = rlt;
+      P.rel_cnt[t] = rcnt;
+    }
+  }
+}
+
 // ------------------------------------------------------------ KC / KP pair products
 // Workgroup (p, g): p = a leading sorted position of a 16-positive tile of
 // one relation (other positions exit at once), g = a group of 4 of the
@@ -209,20 +251,42 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
       }
     }
   }
-  const float* Rm = P.rel.row(r);
-  float* G = P.grel + r * (int64_t)d * d;
-  float n2 = 0.f;
+  // epilogue: the strip's rows [i0, i0 + 16) are one contiguous run of
+  // 16 d floats in both R_r and dR_r, so the accumulators go through LDS and
+  // the run is read / written a float4 per lane (most workgroups -- relations
+  // absent from the batch -- do nothing else: their strip is dense_rel * R_r)
+  const float* Rm = P.rel.row(r) + (int64_t)i0 * d;
+  float* G = P.grel + r * (int64_t)d * d + (int64_t)i0 * d;
+  float* S = Yc;   // [16][D16]
+  __syncthreads();   // the MFMA loop's last reads of Yc
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int jt = wv + 4 * t;
-    const int col = jt * 16 + (lane & 15);
-    if (jt >= nct || col >= d) continue;
+    if (jt >= nct) continue;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int row = i0 + (lane >> 4) * 4 + g;
-      if (row >= d) continue;
-      const float v = acc[t][g] + P.dense_rel * Rm[(int64_t)row * d + col];
-      G[(int64_t)row * d + col] = v;
+    for (int g = 0; g < 4; ++g) S[((lane >> 4) * 4 + g) * D16 + jt * 16 + (lane & 15)] = acc[t][g];
+  }
+  __syncthreads();
+  const int run = min(16, d - i0) * d;
+  float n2 = 0.f;
+  if (d % 4 == 0 && P.rel.ld % 4 == 0 && ((uintptr_t)P.rel.p % 16) == 0 && ((uintptr_t)P.grel % 16) == 0) {
+    for (int e = 4 * threadIdx.x; e < run; e += 4 * blockDim.x) {
+      const int row = e / d, col = e - row * d;
+      const float4 m = *reinterpret_cast<const float4*>(Rm + e);
+      const float* s = S + row * D16 + col;
+      float4 v;
+      v.x = s[0] + P.dense_rel * m.x;
+      v.y = s[1] + P.dense_rel * m.y;
+      v.z = s[2] + P.dense_rel * m.z;
+      v.w = s[3] + P.dense_rel * m.w;
+      *reinterpret_cast<float4*>(G + e) = v;
+      n2 += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+  } else {
+    for (int e = threadIdx.x; e < run; e += blockDim.x) {
+      const int row = e / d, col = e - row * d;
+      const float v = S[row * D16 + col] + P.dense_rel * Rm[e];
+      G[e] = v;
       n2 += v * v;
     }
   }
@@ -340,7 +404,10 @@ __global__ __launch_bounds__(256) void reg_loss_kernel(TabView ent, TabView rel,
 // ------------------------------------------------------------ launchers
 void launch_rel_rank(const RelArgs& P, hipStream_t st) {
   const int64_t n = std::max<int64_t>(P.B, P.rel.rows);
-  hipLaunchKernelGGL(rel_rank_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P);
+  if (n <= 8192)   // wave per item: n * B / 64 lane-loads, all in parallel
+    hipLaunchKernelGGL(rel_rank_wave_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, P);
+  else
+    hipLaunchKernelGGL(rel_rank_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P);
 }
 static unsigned pair_grid(const RelArgs& P) {
   const int nct = (P.d + 15) / 16;
