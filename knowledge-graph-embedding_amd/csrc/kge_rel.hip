@@ -131,7 +131,11 @@ __global__ __launch_bounds__(256) void rel_rank_wave_kernel(RelArgs P) {
 template <int MODE>
 __global__ __launch_bounds__(256) void rel_pair_kernel(RelArgs P) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int d = P.d, D4 = (d + 3) & ~3, nct = (d + 15) / 16;
+  // rows staged at DP = d rounded to 16 floats (zero padded): the MFMA inner
+  // dimension is split into 4 contiguous blocks of DP / 4 (a multiple of 4),
+  // lane group kq = lane >> 4 owning block kq, so a lane's B fragment of the
+  // transposed product (R^T) is a contiguous run of R's row -> float4 loads
+  const int d = P.d, DP = (d + 15) & ~15, nct = (d + 15) / 16;
   const int njg = (2 * nct + 3) / 4;
   const int64_t p = blockIdx.x / njg;
   const int g = (int)(blockIdx.x % njg);
@@ -140,48 +144,64 @@ __global__ __launch_bounds__(256) void rel_pair_kernel(RelArgs P) {
   if ((p - g0) % 16 != 0) return;
   const int n = (int)min<int64_t>(16, g0 + P.rel_cnt[r] - p);
   float* X1 = sm;
-  float* X2 = sm + 16 * D4;
+  float* X2 = sm + 16 * DP;
   __shared__ int64_t s_i[16];
-  if (threadIdx.x < 16) s_i[threadIdx.x] = threadIdx.x < n ? P.sorted[p + threadIdx.x] : 0;
-  __syncthreads();
-  for (int e = threadIdx.x; e < 16 * D4; e += blockDim.x) {
-    const int q = e / D4, k = e - q * D4;
-    float x1 = 0.f, x2 = 0.f;
-    if (q < n && k < d) {
-      const int64_t i = s_i[q];
-      if (MODE == 0) {
-        x1 = P.ent.row(pos_id(P, i, 0))[k];
-        x2 = P.ent.row(pos_id(P, i, 2))[k];
-      } else {
-        const float* gr = P.gpos + i * 3 * (int64_t)P.gcols;
-        x1 = gr[2 * P.gcols + k];   // B_i
-        x2 = gr[k];                 // A_i
-      }
+  __shared__ const float* s_x1[16];
+  __shared__ const float* s_x2[16];
+  if (threadIdx.x < 16) {   // each staged row's source, resolved once
+    const int q = threadIdx.x;
+    const int64_t i = q < n ? P.sorted[p + q] : 0;
+    s_i[q] = i;
+    if (MODE == 0) {
+      s_x1[q] = P.ent.row(pos_id(P, i, 0));
+      s_x2[q] = P.ent.row(pos_id(P, i, 2));
+    } else {
+      const float* gr = P.gpos + i * 3 * (int64_t)P.gcols;
+      s_x1[q] = gr + 2 * P.gcols;   // B_i
+      s_x2[q] = gr;                 // A_i
     }
-    X1[e] = x1;
-    X2[e] = x2;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 16 * DP; e += blockDim.x) {
+    const int q = e / DP, k = e - q * DP;
+    const bool in = q < n && k < d;
+    X1[e] = in ? s_x1[q][k] : 0.f;
+    X2[e] = in ? s_x2[q][k] : 0.f;
   }
   const int lane = lane_id(), wv = wave_id();
   const int job = g * 4 + wv;
   const bool has_job = job < 2 * nct;
   const int prod = job & 1, jt = job >> 1;
   const int col = jt * 16 + (lane & 15), kq = lane >> 4;
-  const int nks = D4 / 4;
+  const int nks = DP / 4;          // k-steps; step ks of lane group kq is k = kq * nks + ks
+  const int kb = kq * nks;
   const float* Rm = P.rel.row(r);
+  const bool v4 = d % 4 == 0 && P.rel.ld % 4 == 0 && ((uintptr_t)P.rel.p % 16) == 0;
   float bf[64];   // d <= 256 (plan check)
+  if (prod == 1 && v4) {
+    // R^T: B[k][col] = R[col][k], a contiguous run of row col
 #pragma unroll
-  for (int ks = 0; ks < 64; ++ks) {
-    const int k = ks * 4 + kq;
-    bf[ks] = (has_job && ks < nks && k < d && col < d)
-                 ? (prod == 0 ? Rm[(int64_t)k * d + col] : Rm[(int64_t)col * d + k]) : 0.f;
+    for (int q4 = 0; q4 < 16; ++q4) {
+      const int k = kb + 4 * q4;   // d % 4 == 0: the 4 elements are all < d or all >= d
+      const float4 x = (has_job && 4 * q4 < nks && k < d && col < d)
+                           ? *reinterpret_cast<const float4*>(Rm + (int64_t)col * d + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      bf[4 * q4] = x.x; bf[4 * q4 + 1] = x.y; bf[4 * q4 + 2] = x.z; bf[4 * q4 + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < 64; ++ks) {
+      const int k = kb + ks;
+      bf[ks] = (has_job && ks < nks && k < d && col < d)
+                   ? (prod == 0 ? Rm[(int64_t)k * d + col] : Rm[(int64_t)col * d + k]) : 0.f;
+    }
   }
   __syncthreads();
   if (!has_job) return;
-  const float* xa = (prod ? X2 : X1) + (lane & 15) * D4 + kq;
+  const float* xa = (prod ? X2 : X1) + (lane & 15) * DP + kb;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 64; ++ks)
-    if (ks < nks) acc = mfma16(xa[ks * 4], bf[ks], acc);
+    if (ks < nks) acc = mfma16(xa[ks], bf[ks], acc);
   if (col < d) {
 #pragma unroll
     for (int gg = 0; gg < 4; ++gg) {
@@ -209,9 +229,23 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
   const int lane = lane_id(), wv = wave_id();
   float* Xc = sm;             // [32][16]
   float* Yc = sm + 32 * 16;   // [32][D16]
-  __shared__ int64_t s_i[16];
+  __shared__ const float* s_x[32];
+  __shared__ const float* s_y[32];
   __shared__ float s_n2[4];
   __shared__ int s_last;
+  // the strip's rows [i0, i0 + 16) are one contiguous run of 16 d floats in
+  // both R_r and dR_r: its R_r part (<= 4 float4 per thread, d <= 256) is
+  // requested first, under the list lookup and the MFMA loop
+  const int run = min(16, d - i0) * d;
+  const float* Rm = P.rel.row(r) + (int64_t)i0 * d;
+  const bool v4 = d % 4 == 0 && P.rel.ld % 4 == 0 && ((uintptr_t)P.rel.p % 16) == 0 && ((uintptr_t)P.grel % 16) == 0;
+  constexpr int kRunV = 16 * 256 / 4 / 256;
+  float4 m[kRunV];
+#pragma unroll
+  for (int k = 0; k < kRunV; ++k) {
+    const int e = 4 * (threadIdx.x + k * 256);
+    m[k] = (v4 && e < run) ? *reinterpret_cast<const float4*>(Rm + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   const int64_t beg = P.rel_beg[r], end = beg + P.rel_cnt[r];
   f32x4 acc[4];
 #pragma unroll
@@ -219,25 +253,26 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
   for (int64_t c0 = beg; c0 < end; c0 += 16) {
     const int nrow = (int)min<int64_t>(16, end - c0);
     __syncthreads();
-    if (threadIdx.x < 16) s_i[threadIdx.x] = threadIdx.x < nrow ? P.sorted[c0 + threadIdx.x] : 0;
+    if (threadIdx.x < 32) {   // each staged row's source, resolved once: h | b rows, A | t rows
+      const int q = threadIdx.x & 15;
+      const int64_t i = q < nrow ? P.sorted[c0 + q] : 0;
+      const float* gr = P.gpos + i * 3 * (int64_t)P.gcols;
+      if (threadIdx.x < 16) {
+        s_x[q] = P.ent.row(pos_id(P, i, 0));
+        s_y[q] = gr;
+      } else {
+        s_x[16 + q] = gr + P.gcols;
+        s_y[16 + q] = P.ent.row(pos_id(P, i, 2));
+      }
+    }
     __syncthreads();
     for (int e = threadIdx.x; e < 32 * 16; e += blockDim.x) {
       const int q = e >> 4, c = i0 + (e & 15);
-      float x = 0.f;
-      if ((q & 15) < nrow && c < d) {
-        const int64_t i = s_i[q & 15];
-        x = q < 16 ? P.ent.row(pos_id(P, i, 0))[c] : P.gpos[i * 3 * (int64_t)P.gcols + P.gcols + c];   // h | b
-      }
-      Xc[e] = x;
+      Xc[e] = ((q & 15) < nrow && c < d) ? s_x[q][c] : 0.f;
     }
     for (int e = threadIdx.x; e < 32 * D16; e += blockDim.x) {
       const int q = e / D16, c = e - q * D16;
-      float y = 0.f;
-      if ((q & 15) < nrow && c < d) {
-        const int64_t i = s_i[q & 15];
-        y = q < 16 ? P.gpos[i * 3 * (int64_t)P.gcols + c] : P.ent.row(pos_id(P, i, 2))[c];   // A | t
-      }
-      Yc[e] = y;
+      Yc[e] = ((q & 15) < nrow && c < d) ? s_y[q][c] : 0.f;
     }
     __syncthreads();
 #pragma unroll
@@ -251,11 +286,9 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
       }
     }
   }
-  // epilogue: the strip's rows [i0, i0 + 16) are one contiguous run of
-  // 16 d floats in both R_r and dR_r, so the accumulators go through LDS and
-  // the run is read / written a float4 per lane (most workgroups -- relations
-  // absent from the batch -- do nothing else: their strip is dense_rel * R_r)
-  const float* Rm = P.rel.row(r) + (int64_t)i0 * d;
+  // epilogue: the accumulators go through LDS and the run is written a float4
+  // per lane (most workgroups -- relations absent from the batch -- do
+  // nothing else: their strip is dense_rel * R_r)
   float* G = P.grel + r * (int64_t)d * d + (int64_t)i0 * d;
   float* S = Yc;   // [16][D16]
   __syncthreads();   // the MFMA loop's last reads of Yc
@@ -267,18 +300,19 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
     for (int g = 0; g < 4; ++g) S[((lane >> 4) * 4 + g) * D16 + jt * 16 + (lane & 15)] = acc[t][g];
   }
   __syncthreads();
-  const int run = min(16, d - i0) * d;
   float n2 = 0.f;
-  if (d % 4 == 0 && P.rel.ld % 4 == 0 && ((uintptr_t)P.rel.p % 16) == 0 && ((uintptr_t)P.grel % 16) == 0) {
-    for (int e = 4 * threadIdx.x; e < run; e += 4 * blockDim.x) {
+  if (v4) {
+#pragma unroll
+    for (int k = 0; k < kRunV; ++k) {
+      const int e = 4 * (threadIdx.x + k * 256);
+      if (e >= run) continue;
       const int row = e / d, col = e - row * d;
-      const float4 m = *reinterpret_cast<const float4*>(Rm + e);
-      const float* s = S + row * D16 + col;
+      const float* sv = S + row * D16 + col;
       float4 v;
-      v.x = s[0] + P.dense_rel * m.x;
-      v.y = s[1] + P.dense_rel * m.y;
-      v.z = s[2] + P.dense_rel * m.z;
-      v.w = s[3] + P.dense_rel * m.w;
+      v.x = sv[0] + P.dense_rel * m[k].x;
+      v.y = sv[1] + P.dense_rel * m[k].y;
+      v.z = sv[2] + P.dense_rel * m[k].z;
+      v.w = sv[3] + P.dense_rel * m[k].w;
       *reinterpret_cast<float4*>(G + e) = v;
       n2 += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
     }
@@ -414,11 +448,11 @@ static unsigned pair_grid(const RelArgs& P) {
   return (unsigned)(P.B * ((2 * nct + 3) / 4));
 }
 void launch_rel_ctx(const RelArgs& P, hipStream_t st) {
-  const size_t lds = 2 * 16 * (size_t)((P.d + 3) & ~3) * sizeof(float);
+  const size_t lds = 2 * 16 * (size_t)((P.d + 15) & ~15) * sizeof(float);
   hipLaunchKernelGGL(rel_pair_kernel<0>, dim3(pair_grid(P)), dim3(256), lds, st, P);
 }
 void launch_rel_post(const RelArgs& P, hipStream_t st) {
-  const size_t lds = 2 * 16 * (size_t)((P.d + 3) & ~3) * sizeof(float);
+  const size_t lds = 2 * 16 * (size_t)((P.d + 15) & ~15) * sizeof(float);
   hipLaunchKernelGGL(rel_pair_kernel<1>, dim3(pair_grid(P)), dim3(256), lds, st, P);
   const int nct = (P.d + 15) / 16;
   const size_t lds2 = (32 * 16 + 32 * (size_t)nct * 16) * sizeof(float);
