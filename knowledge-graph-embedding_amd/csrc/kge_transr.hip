@@ -165,15 +165,25 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
   const float* Mr = T.proj.row(pr);
   {
     const int nct = (k + 15) / 16, nkc = (LX - 1) / 16, nrt = L.NR16 / 16;
-    for (int ct = wv; ct < nct; ct += kTrWaves) {
+    // jobs = (column tile, row-tile pair), column-major, dealt to the waves in
+    // equal contiguous ranges (13 column tiles over 8 waves left two SIMDs
+    // with a third more work); B is reloaded only when the column tile changes
+    const int npr = (nrt + 1) / 2, nj = nct * npr;
+    const int jb = wv * nj / kTrWaves, je = (wv + 1) * nj / kTrWaves;
+    int cur = -1;
+    float bf[kTrKS];
+    for (int jo = jb; jo < je; ++jo) {
+      const int ct = jo / npr, rt = (jo - ct * npr) * 2;
       const int col = ct * 16 + (lane & 15);
-      float bf[kTrKS];
+      if (ct != cur) {
+        cur = ct;
 #pragma unroll
-      for (int ks = 0; ks < kTrKS; ++ks) {
-        const int kk = ks * 4 + (lane >> 4);
-        bf[ks] = (kk < d && col < k) ? Mr[(int64_t)kk * k + col] : 0.f;
+        for (int ks = 0; ks < kTrKS; ++ks) {
+          const int kk = ks * 4 + (lane >> 4);
+          bf[ks] = (kk < d && col < k) ? Mr[(int64_t)kk * k + col] : 0.f;
+        }
       }
-      for (int rt = 0; rt < nrt; rt += 2) {
+      {
         const int rt1 = rt + 1 < nrt ? rt + 1 : rt;   // odd count: the last tile twice (discarded)
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
         const float* x0 = X + (rt * 16 + (lane & 15)) * LX + (lane >> 4);
@@ -434,15 +444,23 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
     {
       const int nct = (d + 15) / 16, nkc = (LP - 1) / 16, nrt = (NS + 15) / 16;
       float* gp2 = gp;
-      for (int ct = wv; ct < nct; ct += kTrWaves) {
+      // (column tile, row-tile pair) jobs in equal contiguous ranges, as GEMM1
+      const int npr = (nrt + 1) / 2, nj = nct * npr;
+      const int jb = wv * nj / kTrWaves, je = (wv + 1) * nj / kTrWaves;
+      int cur = -1;
+      float bf[kTrKS];
+      for (int jo = jb; jo < je; ++jo) {
+        const int ct = jo / npr, rt = (jo - ct * npr) * 2;
         const int col = ct * 16 + (lane & 15);
-        float bf[kTrKS];
+        if (ct != cur) {
+          cur = ct;
 #pragma unroll
-        for (int ks = 0; ks < kTrKS; ++ks) {
-          const int kk = ks * 4 + (lane >> 4);
-          bf[ks] = (kk < k && col < d) ? Mr[(int64_t)col * k + kk] : 0.f;
+          for (int ks = 0; ks < kTrKS; ++ks) {
+            const int kk = ks * 4 + (lane >> 4);
+            bf[ks] = (kk < k && col < d) ? Mr[(int64_t)col * k + kk] : 0.f;
+          }
         }
-        for (int rt = 0; rt < nrt; rt += 2) {
+        {
           const int rt1 = rt + 1 < nrt ? rt + 1 : rt;
           f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
           const float* s0 = S + (rt * 16 + (lane & 15)) * LP + (lane >> 4);
@@ -475,15 +493,24 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
     {
       const int nrt = (d + 15) / 16, nct = (k + 15) / 16, nkc = (NR + 15) / 16;
       float* dm = T.dmpart + i * (int64_t)d * k;
-      for (int rt = wv; rt < nrt; rt += kTrWaves) {
+      // (row tile, column-tile pair) jobs in equal contiguous ranges; the A
+      // column is reloaded only when the row tile changes
+      const int npc = (nct + 1) / 2, nj = nrt * npc;
+      const int jb = wv * nj / kTrWaves, je = (wv + 1) * nj / kTrWaves;
+      int cur = -1;
+      float af[kTrKS3];
+      for (int jo = jb; jo < je; ++jo) {
+        const int rt = jo / npc, ct = (jo - rt * npc) * 2;
         const int ci = rt * 16 + (lane & 15);
-        float af[kTrKS3];
+        if (rt != cur) {
+          cur = rt;
 #pragma unroll
-        for (int ks = 0; ks < kTrKS3; ++ks) {
-          const int kk = ks * 4 + (lane >> 4);
-          af[ks] = (kk < NR && ci < d) ? A.ent.row(row_id(kk))[ci] : 0.f;
+          for (int ks = 0; ks < kTrKS3; ++ks) {
+            const int kk = ks * 4 + (lane >> 4);
+            af[ks] = (kk < NR && ci < d) ? A.ent.row(row_id(kk))[ci] : 0.f;
+          }
         }
-        for (int ct = 0; ct < nct; ct += 2) {
+        {
           const int ct1 = ct + 1 < nct ? ct + 1 : ct;
           f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
           const float* b0 = S + (lane >> 4) * LP + ct * 16 + (lane & 15);
