@@ -228,11 +228,10 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
   const int ti = (int)(blockIdx.x % nct), i0 = ti * 16;
   const int lane = lane_id(), wv = wave_id();
   float* Xc = sm;             // [32][16]
-  float* Yc = sm + 32 * 16;   // [32][D16]
+  float* Yc = sm + 32 * 16;   // [16][D16]
   __shared__ const float* s_x[32];
   __shared__ const float* s_y[32];
   __shared__ float s_n2[4];
-  __shared__ int s_last;
   // the strip's rows [i0, i0 + 16) are one contiguous run of 16 d floats in
   // both R_r and dR_r: its R_r part (<= 4 float4 per thread, d <= 256) is
   // requested first, under the list lookup and the MFMA loop
@@ -270,19 +269,25 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
       const int q = e >> 4, c = i0 + (e & 15);
       Xc[e] = ((q & 15) < nrow && c < d) ? s_x[q][c] : 0.f;
     }
-    for (int e = threadIdx.x; e < 32 * D16; e += blockDim.x) {
-      const int q = e / D16, c = e - q * D16;
-      Yc[e] = ((q & 15) < nrow && c < d) ? s_y[q][c] : 0.f;
-    }
-    __syncthreads();
+    // Y in two halves through one [16][D16] buffer (A rows for k < 16, then
+    // t rows): half the LDS, so twice the workgroups per CU; same k order
 #pragma unroll
-    for (int k0 = 0; k0 < 32; k0 += 4) {
-      const int k = k0 + (lane >> 4);
-      const float a = Xc[k * 16 + (lane & 15)];
+    for (int half = 0; half < 2; ++half) {
+      if (half) __syncthreads();   // the first half's MFMA reads of Yc
+      for (int e = threadIdx.x; e < 16 * D16; e += blockDim.x) {
+        const int q = e / D16, c = e - q * D16;
+        Yc[e] = (q < nrow && c < d) ? s_y[16 * half + q][c] : 0.f;
+      }
+      __syncthreads();
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int jt = wv + 4 * t;
-        if (jt < nct) acc[t] = mfma16(a, Yc[k * D16 + jt * 16 + (lane & 15)], acc[t]);
+      for (int k0 = 0; k0 < 16; k0 += 4) {
+        const int k = k0 + (lane >> 4);
+        const float a = Xc[(16 * half + k) * 16 + (lane & 15)];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int jt = wv + 4 * t;
+          if (jt < nct) acc[t] = mfma16(a, Yc[k * D16 + jt * 16 + (lane & 15)], acc[t]);
+        }
       }
     }
   }
@@ -327,27 +332,24 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
   n2 = wave_sum(n2);
   if (lane == 0) s_n2[wv] = n2;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const float w = s_n2[0] + s_n2[1] + s_n2[2] + s_n2[3];
-    __hip_atomic_store(&P.rpart[blockIdx.x], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_s_waitcnt(0);
-    const uint32_t prev = __hip_atomic_fetch_add(&P.ctl->rel_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = prev == gridDim.x - 1;
-  }
+  // the strip's norm^2 partial; rel_dr_norm_kernel (next launch on the
+  // stream) sums them in a fixed order -- no grid-wide ticket: 3 k workgroups
+  // taking turns on one counter cost more than the extra launch
+  if (threadIdx.x == 0) P.rpart[blockIdx.x] = s_n2[0] + s_n2[1] + s_n2[2] + s_n2[3];
+}
+
+__global__ __launch_bounds__(256) void rel_dr_norm_kernel(RelArgs P, int n) {
+  __shared__ float s_n2[4];
+  const int lane = lane_id(), wv = wave_id();
+  float s = 0.f;
+  for (int w = threadIdx.x; w < n; w += blockDim.x) s += P.rpart[w];
+  s = wave_sum(s);
+  if (lane == 0) s_n2[wv] = s;
   __syncthreads();
-  if (s_last) {
-    float s = 0.f;
-    for (int w = threadIdx.x; w < (int)gridDim.x; w += blockDim.x)
-      s += __hip_atomic_load(&P.rpart[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s = wave_sum(s);
-    if (lane == 0) s_n2[wv] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const float t = s_n2[0] + s_n2[1] + s_n2[2] + s_n2[3];
-      P.ctl->dn2[1] = t;
-      if (P.norm2_out) P.norm2_out[1] = t;
-      P.ctl->rel_ticket = 0u;
-    }
+  if (threadIdx.x == 0) {
+    const float t = s_n2[0] + s_n2[1] + s_n2[2] + s_n2[3];
+    P.ctl->dn2[1] = t;
+    if (P.norm2_out) P.norm2_out[1] = t;
   }
 }
 
@@ -455,8 +457,9 @@ void launch_rel_post(const RelArgs& P, hipStream_t st) {
   const size_t lds = 2 * 16 * (size_t)((P.d + 15) & ~15) * sizeof(float);
   hipLaunchKernelGGL(rel_pair_kernel<1>, dim3(pair_grid(P)), dim3(256), lds, st, P);
   const int nct = (P.d + 15) / 16;
-  const size_t lds2 = (32 * 16 + 32 * (size_t)nct * 16) * sizeof(float);
+  const size_t lds2 = (32 * 16 + 16 * (size_t)nct * 16) * sizeof(float);
   hipLaunchKernelGGL(rel_dr_kernel, dim3((unsigned)(P.rel.rows * nct)), dim3(256), lds2, st, P);
+  hipLaunchKernelGGL(rel_dr_norm_kernel, dim3(1), dim3(256), 0, st, P, (int)(P.rel.rows * nct));
 }
 void launch_reg_loss(const TabView& ent, const TabView& rel, float lam, float* part, StepCtl* ctl,
                      float* loss_out, float* loss_accum, hipStream_t st) {
