@@ -1064,12 +1064,12 @@ void update_kernel(StepArgs A) {
     }
   }
   if (A.dense) {
-    // ||dense gradient||^2: workgroup partial, the last workgroup reduces
-    // every partial in a fixed order (clip_by_norm of the dense tensor)
+    // ||dense gradient||^2: workgroup partial; partials_norm_kernel (the next
+    // launch) sums them in a fixed order (clip_by_norm of the dense tensor) --
+    // no ticket on one counter from every workgroup
     // (in the sort scratch: 20 bytes of their own would cost a workgroup of
     // occupancy -- 7 instead of 8 per CU at 20,480 bytes of LDS each)
     float* s_n2 = reinterpret_cast<float*>(&s_scr[0][0]);
-    int* s_lastu = reinterpret_cast<int*>(&s_scr[0][kUpdWaves]);
     __syncthreads();   // every wave is done with its scratch
     dn2 = wave_sum(dn2);
     if (lane == 0) s_n2[wv] = dn2;
@@ -1077,26 +1077,7 @@ void update_kernel(StepArgs A) {
     if (threadIdx.x == 0) {
       float w = 0.f;
       for (int k = 0; k < kUpdWaves; ++k) w += s_n2[k];
-      __hip_atomic_store(&A.upart[blockIdx.x], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_waitcnt(0);
-      const uint32_t prev = __hip_atomic_fetch_add(&A.ctl->upd_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *s_lastu = prev == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (*s_lastu) {
-      float acc2 = 0.f;
-      for (int w = threadIdx.x; w < (int)gridDim.x; w += blockDim.x)
-        acc2 += __hip_atomic_load(&A.upart[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      acc2 = wave_sum(acc2);
-      if (lane == 0) s_n2[wv] = acc2;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        float t = 0.f;
-        for (int k = 0; k < kUpdWaves; ++k) t += s_n2[k];
-        A.ctl->dn2[0] = t;
-        if (A.norm2_out) A.norm2_out[0] = t;
-        A.ctl->upd_ticket = 0u;
-      }
+      A.upart[blockIdx.x] = w;
     }
   }
   KGE_PROF(16);

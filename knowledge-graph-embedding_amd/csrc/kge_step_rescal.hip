@@ -5,6 +5,24 @@
 namespace kge {
 
 #ifndef KGE_ONLY_ONE
+// Fixed-order sum of n per-workgroup norm^2 partials into ctl->dn2[slot]
+// (and norm2_out[slot]): one workgroup, launched right after the producer.
+__global__ __launch_bounds__(256) void partials_norm_kernel(const float* part, int n, StepCtl* ctl, int slot,
+                                                            float* norm2_out) {
+  __shared__ float s_n2[4];
+  const int lane = lane_id(), wv = wave_id();
+  float s = 0.f;
+  for (int w = threadIdx.x; w < n; w += blockDim.x) s += part[w];
+  s = wave_sum(s);
+  if (lane == 0) s_n2[wv] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = s_n2[0] + s_n2[1] + s_n2[2] + s_n2[3];
+    ctl->dn2[slot] = t;
+    if (norm2_out) norm2_out[slot] = t;
+  }
+}
+
 // RESCAL: context pass -> score (dot products against u / v) -> regulariser
 // loss -> projection + dR pass -> update kernel (dense entity gradient)
 template <int VEC, int NC>
@@ -18,6 +36,7 @@ static kge_status rescal_vn(const StepArgs& A, const StepGeom& G, const RelArgs&
   if (A.train) {
     launch_rel_post(P, st);
     hipLaunchKernelGGL((update_kernel<Rescal, VEC, NC, SK_DOT>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
+    hipLaunchKernelGGL(partials_norm_kernel, dim3(1), dim3(256), 0, st, A.upart, (int)G.gridU, A.ctl, 0, A.norm2_out);
   }
   return KGE_OK;
 }
