@@ -350,7 +350,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.o_part = take((uint64_t)((transr || proj) ? std::max<int64_t>(nWG, B) : nWG) * 8 * 4);   // one partial per positive
   P.o_list = take((uint64_t)nlists * cap * 4);
   P.o_ovf = take((uint64_t)T * 8);
-  P.o_upart = take((uint64_t)P.G.gridU * 4);
+  P.o_upart = take((uint64_t)P.G.gridU * 2 * 4);   // gradient norm^2 | entity norm^2 (dense mode)
   P.o_leaders = take((uint64_t)(compact ? (int64_t)P.G.gridU * kUpdWaves : 1) * 16);
   P.hbits = hbits;
   if (rescal) {
@@ -358,7 +358,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     P.o_sorted = take((uint64_t)B * 4);
     P.o_srel = take((uint64_t)B * 4);
     P.o_gproj = take((uint64_t)B * 2 * entc * 4);
-    P.o_rpart = take((uint64_t)R * nct * 4);
+    P.o_rpart = take((uint64_t)R * nct * 2 * 4);   // gradient norm^2 | ||R||^2 per strip
     P.o_regpart = take((uint64_t)kRegWGs * 2 * 4);
     if (d->optimizer == KGE_OPT_SGD) {   // dense gradients (KGE_OPT_GRAD: the caller's grad_out)
       P.o_gent = take((uint64_t)E * entc * 4);

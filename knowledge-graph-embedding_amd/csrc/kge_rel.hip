@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
   float* Yc = sm + 32 * 16;   // [16][D16]
   __shared__ const float* s_x[32];
   __shared__ const float* s_y[32];
-  __shared__ float s_n2[4];
+  __shared__ float s_n2[4], s_m2[4];
   // the strip's rows [i0, i0 + 16) are one contiguous run of 16 d floats in
   // both R_r and dR_r: its R_r part (<= 4 float4 per thread, d <= 256) is
   // requested first, under the list lookup and the MFMA loop
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
     for (int g = 0; g < 4; ++g) S[((lane >> 4) * 4 + g) * D16 + jt * 16 + (lane & 15)] = acc[t][g];
   }
   __syncthreads();
-  float n2 = 0.f;
+  float n2 = 0.f, m2 = 0.f;   // gradient norm^2 | ||R_r||^2 (regulariser loss)
   if (v4) {
 #pragma unroll
     for (int k = 0; k < kRunV; ++k) {
@@ -320,35 +320,48 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
       v.w = sv[3] + P.dense_rel * m[k].w;
       *reinterpret_cast<float4*>(G + e) = v;
       n2 += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+      m2 += m[k].x * m[k].x + m[k].y * m[k].y + m[k].z * m[k].z + m[k].w * m[k].w;
     }
   } else {
     for (int e = threadIdx.x; e < run; e += blockDim.x) {
       const int row = e / d, col = e - row * d;
-      const float v = S[row * D16 + col] + P.dense_rel * Rm[e];
+      const float rm = Rm[e];
+      const float v = S[row * D16 + col] + P.dense_rel * rm;
       G[e] = v;
       n2 += v * v;
+      m2 += rm * rm;
     }
   }
   n2 = wave_sum(n2);
-  if (lane == 0) s_n2[wv] = n2;
+  m2 = wave_sum(m2);
+  if (lane == 0) { s_n2[wv] = n2; s_m2[wv] = m2; }
   __syncthreads();
-  // the strip's norm^2 partial; rel_dr_norm_kernel (next launch on the
-  // stream) sums them in a fixed order -- no grid-wide ticket: 3 k workgroups
-  // taking turns on one counter cost more than the extra launch
-  if (threadIdx.x == 0) P.rpart[blockIdx.x] = s_n2[0] + s_n2[1] + s_n2[2] + s_n2[3];
+  // the strip's partials ([grid] gradient norm^2 | [grid] ||R||^2);
+  // rel_dr_norm_kernel (next launch on the stream) sums them in a fixed
+  // order -- no grid-wide ticket: 3 k workgroups taking turns on one counter
+  // cost more than the extra launch
+  if (threadIdx.x < 2) {
+    const float* q = threadIdx.x ? s_m2 : s_n2;
+    P.rpart[threadIdx.x * gridDim.x + blockIdx.x] = q[0] + q[1] + q[2] + q[3];
+  }
 }
 
 __global__ __launch_bounds__(256) void rel_dr_norm_kernel(RelArgs P, int n) {
-  __shared__ float s_n2[4];
+  __shared__ float s_n2[4], s_m2[4];
   const int lane = lane_id(), wv = wave_id();
-  float s = 0.f;
-  for (int w = threadIdx.x; w < n; w += blockDim.x) s += P.rpart[w];
+  float s = 0.f, m = 0.f;
+  for (int w = threadIdx.x; w < n; w += blockDim.x) {
+    s += P.rpart[w];
+    m += P.rpart[n + w];
+  }
   s = wave_sum(s);
-  if (lane == 0) s_n2[wv] = s;
+  m = wave_sum(m);
+  if (lane == 0) { s_n2[wv] = s; s_m2[wv] = m; }
   __syncthreads();
   if (threadIdx.x == 0) {
     const float t = s_n2[0] + s_n2[1] + s_n2[2] + s_n2[3];
     P.ctl->dn2[1] = t;
+    P.ctl->reg_r2 = s_m2[0] + s_m2[1] + s_m2[2] + s_m2[3];
     if (P.norm2_out) P.norm2_out[1] = t;
   }
 }

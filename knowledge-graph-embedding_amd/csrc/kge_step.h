@@ -38,7 +38,8 @@ struct StepCtl {
   uint32_t rel_ticket;     // relation-matrix gradient workgroups done (rel norm^2)
   uint32_t reg_ticket;     // regulariser-loss workgroups done
   float dn2[4];            // norm^2 of the dense (duplicate-summed) gradient per variable
-  uint32_t pad1[3];
+  float reg_r2;            // RESCAL train step: sum_r ||R_r||_F^2 (rel_dr partials)
+  uint32_t pad1[2];
 };
 
 // Everything a step kernel needs, passed by value (kernarg segment).

@@ -811,6 +811,7 @@ void update_kernel(StepArgs A) {
   };
 
   float dn2 = 0.f;   // dense mode: this wave's ||summed row gradient||^2
+  float en2 = 0.f;   // dense mode: this wave's ||entity row||^2 (the regulariser loss, RESCAL.py:190-198)
   if (active) {
     const bool is_ent = d < E_;
     const uint32_t* lst = A.list + li * (int64_t)A.cap;
@@ -1029,6 +1030,7 @@ void update_kernel(StepArgs A) {
           for (int q = 0; q < VEC * NC; ++q) acc.v[q] += accE * E.v[q];
         }
         if (A.dense) {
+          en2 = sq_partial(E);
 #pragma unroll
           for (int q = 0; q < VEC * NC; ++q) acc.v[q] += A.dense_ent * E.v[q];
           dn2 = sq_partial(acc);
@@ -1072,12 +1074,13 @@ void update_kernel(StepArgs A) {
     float* s_n2 = reinterpret_cast<float*>(&s_scr[0][0]);
     __syncthreads();   // every wave is done with its scratch
     dn2 = wave_sum(dn2);
-    if (lane == 0) s_n2[wv] = dn2;
+    en2 = wave_sum(en2);
+    if (lane == 0) { s_n2[wv] = dn2; s_n2[kUpdWaves + wv] = en2; }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 2) {   // [gridU] gradient norm^2 | [gridU] entity norm^2
       float w = 0.f;
-      for (int k = 0; k < kUpdWaves; ++k) w += s_n2[k];
-      A.upart[blockIdx.x] = w;
+      for (int k = 0; k < kUpdWaves; ++k) w += s_n2[threadIdx.x * kUpdWaves + k];
+      A.upart[threadIdx.x * gridDim.x + blockIdx.x] = w;
     }
   }
   KGE_PROF(16);
