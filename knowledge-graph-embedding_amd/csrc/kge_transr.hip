@@ -612,6 +612,34 @@ __global__ __launch_bounds__(256) void transr_proj_apply(StepArgs A, TrArgs T) {
   if (beg == end) return;
   const float sc = A.ctl->scale[2];
   const int64_t e1 = min(dk, (ch + 1) * 1024);
+  const bool v4 = dk % 4 == 0 && T.proj.ld % 4 == 0 && ((uintptr_t)T.proj.p % 16) == 0 &&
+                  ((uintptr_t)T.dmpart % 16) == 0 && (!T.gproj_out || ((uintptr_t)T.gproj_out % 16) == 0);
+  if (v4) {
+    // a float4 of M_r per thread; the relation's partials four positives at
+    // a time, every load issued before the adds (same ascending order)
+    const int64_t e = ch * 1024 + 4 * (int64_t)threadIdx.x;
+    if (e >= e1) return;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto add = [&](const float4& x) { g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w; };
+    const float* base = T.dmpart + e;
+    int64_t p = beg;
+    for (; p + 4 <= end; p += 4) {
+      float4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const float4*>(base + (int64_t)T.sorted[p + u] * dk);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) add(x[u]);
+    }
+    for (; p < end; ++p) add(*reinterpret_cast<const float4*>(base + (int64_t)T.sorted[p] * dk));
+    if (T.gproj_out) *reinterpret_cast<float4*>(T.gproj_out + r * dk + e) = g;
+    else {
+      float4* w = reinterpret_cast<float4*>(T.proj.p + r * T.proj.ld + e);
+      float4 m = *w;
+      m.x = m.x + g.x * sc; m.y = m.y + g.y * sc; m.z = m.z + g.z * sc; m.w = m.w + g.w * sc;
+      *w = m;
+    }
+    return;
+  }
   for (int64_t e = ch * 1024 + threadIdx.x; e < e1; e += 256) {
     float g = 0.f;
     for (int64_t p = beg; p < end; ++p) g += T.dmpart[(int64_t)T.sorted[p] * dk + e];
