@@ -15,9 +15,18 @@
  *    legacy default stream).
  *  - The library never allocates device memory: the caller passes a
  *    workspace of at least kge_step_workspace_bytes() bytes, ZERO-FILLED when
- *    it is allocated (a fresh workspace must be zeroed once). Between calls it
- *    holds only zeros again: the step's tickets and per-destination counters
- *    reset themselves. One workspace serves one stream at a time.
+ *    it is allocated (a fresh workspace must be zeroed once). Between calls of
+ *    one plan its tickets and per-destination counters reset themselves. One
+ *    workspace serves one stream at a time.
+ *  - The workspace belongs to ONE plan: kge_step_plan_signature() (a hash of
+ *    the workspace layout -- model, batch, negatives, table shapes, optimizer
+ *    mode, flags) is stamped into the workspace's control block by the first
+ *    step that uses it. A step whose plan differs from the stamped one (the
+ *    caller changed batch size, tables, ... and reused the buffer without
+ *    re-zeroing it) is REFUSED on the device: none of its kernels writes a
+ *    table or an output, the status word gets KGE_EWORKSPACE and *loss_out is
+ *    NaN. Re-zero the workspace (or allocate a zeroed one) whenever the
+ *    signature changes.
  *  - Calls are stream-ordered, re-entrant and never throw. They return a
  *    kge_status; kge_last_error() gives a thread-local message.
  *  - Device-side range violations (entity / relation ids out of range) are
@@ -35,7 +44,7 @@
 extern "C" {
 #endif
 
-#define KGE_ABI_VERSION 4
+#define KGE_ABI_VERSION 5
 
 typedef enum kge_status {
   KGE_OK = 0,
@@ -43,7 +52,8 @@ typedef enum kge_status {
   KGE_ERANGE = 2,            /* id out of range (reference: TF gather InvalidArgument on CPU) */
   KGE_EHIP = 3,              /* HIP runtime error */
   KGE_ENOMEM_WORKSPACE = 4,  /* workspace smaller than kge_step_workspace_bytes() */
-  KGE_EUNSUPPORTED = 5       /* combination not implemented natively */
+  KGE_EUNSUPPORTED = 5,      /* combination not implemented natively */
+  KGE_EWORKSPACE = 6         /* device status: workspace stamped by another plan (step refused) */
 } kge_status;
 
 /* models: KGE/models/translating_based/<Model>.py, KGE/models/semantic_based/<Model>.py */
@@ -365,6 +375,11 @@ const char* kge_last_error(void);
 
 /* Workspace needed by kge_step for this descriptor (0 on error). */
 uint64_t kge_step_workspace_bytes(const kge_step_desc* d);
+
+/* Signature of the workspace layout this descriptor's plan uses (never 0;
+ * 0 on error): a workspace stamped with another value must be re-zeroed
+ * before this plan uses it (see the ABI rules above). */
+uint32_t kge_step_plan_signature(const kge_step_desc* d);
 
 /* One training / validation step (see kge_step_desc). */
 kge_status kge_step(const kge_step_desc* d, void* stream);

@@ -11,9 +11,9 @@ import threading
 
 import torch
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
-KGE_OK, KGE_EINVAL, KGE_ERANGE, KGE_EHIP, KGE_ENOMEM_WORKSPACE, KGE_EUNSUPPORTED = range(6)
+KGE_OK, KGE_EINVAL, KGE_ERANGE, KGE_EHIP, KGE_ENOMEM_WORKSPACE, KGE_EUNSUPPORTED, KGE_EWORKSPACE = range(7)
 
 MODEL_TRANSE, MODEL_TRANSH, MODEL_TRANSR, MODEL_TRANSD, MODEL_ROTATE, MODEL_DISTMULT, MODEL_RESCAL = range(7)
 SIDE_H, SIDE_T, SIDE_HT = range(3)
@@ -107,7 +107,8 @@ class kge_stream_desc(ctypes.Structure):
                 ("out", ctypes.c_void_p)]
 
 
-EXPORTS = ("kge_abi_version", "kge_last_error", "kge_step_workspace_bytes", "kge_step", "kge_sample",
+EXPORTS = ("kge_abi_version", "kge_last_error", "kge_step_workspace_bytes", "kge_step_plan_signature", "kge_step",
+           "kge_sample",
            "kge_apply", "kge_constrain_rows", "kge_rank", "kge_apply_rows", "kge_stream_batch")
 
 _lock = threading.Lock()
@@ -129,6 +130,8 @@ def load(path=LIB_PATH):
         L.kge_last_error.restype = ctypes.c_char_p
         L.kge_step_workspace_bytes.restype = ctypes.c_uint64
         L.kge_step_workspace_bytes.argtypes = [ctypes.POINTER(kge_step_desc)]
+        L.kge_step_plan_signature.restype = ctypes.c_uint32
+        L.kge_step_plan_signature.argtypes = [ctypes.POINTER(kge_step_desc)]
         L.kge_step.restype = ctypes.c_int
         L.kge_step.argtypes = [ctypes.POINTER(kge_step_desc), ctypes.c_void_p]
         L.kge_sample.restype = ctypes.c_int
@@ -176,6 +179,9 @@ def check_device_status(status_tensor, what="kge"):
     if code == KGE_EINVAL:
         raise ValueError("%s: a typed-sampling pool is empty after removing the entity itself "
                          "(np.random.choice on an empty pool, utils.py:11-16)" % what)
+    if code == KGE_EWORKSPACE:
+        raise RuntimeError("%s: the step was refused: its workspace was last used by a different plan and was "
+                           "not re-zeroed (kge_hip.h workspace rules); tables and outputs are unchanged" % what)
     raise RuntimeError("%s: device status %d" % (what, code))
 
 

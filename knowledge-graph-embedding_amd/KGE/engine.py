@@ -43,8 +43,9 @@ def device():
 _SIDE = {"h": _hip.SIDE_H, "t": _hip.SIDE_T, "h+t": _hip.SIDE_HT}
 
 
-def fused_plan(model, optimizer):
-    """Return None if (model, plugins, optimizer) run in ``kge_step``, else a reason."""
+def fused_plan(model, optimizer, batch_size=1):
+    """Return None if (model, plugins, optimizer) run in ``kge_step`` for
+    batches of ``batch_size`` triples, else a reason."""
     if backend() == "eager":
         return "KGE_BACKEND=eager"
     if getattr(model, "_fused_model_id", None) is None:
@@ -63,21 +64,24 @@ def fused_plan(model, optimizer):
         return "custom negative sampler"
     if optimizer is not None and not isinstance(optimizer, (_opt.SGD, _opt.Adam)):
         return "%s optimizer has no fused apply" % type(optimizer).__name__
-    return _native_plan_error(model, optimizer)
+    return _native_plan_error(model, optimizer, batch_size)
 
 
-def _native_plan_error(model, optimizer):
+def _native_plan_error(model, optimizer, batch_size=1):
     """Ask the library whether it has an instance for this combination
     (``kge_step_workspace_bytes`` is 0 for a plan it cannot run, with the
     reason in ``kge_last_error``: rows wider than the fragment limit, LDS
-    budget, RESCAL without its regulariser, ...). Cached per configuration."""
+    budget, RESCAL without its regulariser, 32-bit destination codes, ...),
+    with the real batch size and the optimizer's step mode (SGD in-step, Adam
+    as KGE_OPT_GRAD). Cached per configuration."""
     try:
         t = model._fused_tables()
     except (AttributeError, KeyError):
         return None
     if t["ent"].device.type != "cuda":
         return None      # FusedStep raises: the fused step needs the model on a GPU
-    key = (tuple(t["ent"].shape), tuple(t["rel"].shape), type(optimizer).__name__, model.negative_ratio,
+    key = (int(batch_size), tuple(t["ent"].shape), tuple(t["rel"].shape), type(optimizer).__name__,
+           model.negative_ratio,
            model.corrupt_side, bool(getattr(model, "constraint", False)),
            _score.fused_descriptor(model.score_fn) if hasattr(model, "score_fn") else None,
            _loss.fused_descriptor(model.loss_fn))
@@ -86,12 +90,18 @@ def _native_plan_error(model, optimizer):
         lib = _hip.lib()      # raises if libkge_hip.so is missing (no silent fallback)
         probe = FusedStep(model)
         dev = t["ent"].device
-        batch = torch.zeros((1, 3), dtype=torch.int64, device=dev)
-        neg = torch.zeros(max(int(model.negative_ratio), 1), dtype=torch.int64, device=dev)
+        B = max(int(batch_size), 1)
+        batch = torch.zeros((B, 3), dtype=torch.int64, device=dev)
         train = optimizer is not None
-        # the SGD form of the plan (an Adam probe would allocate dense gradients)
+        # the SGD descriptor, switched to the gradient mode for Adam: the plan
+        # check reads no buffer, so non-null placeholders stand in for the
+        # dense gradient outputs (a probe must not allocate E x cols floats)
         opt = optimizer if isinstance(optimizer, _opt.SGD) or not train else _opt.SGD(0.01)
-        d = probe.describe(batch, train, opt, neg_ids=neg)
+        d = probe.describe(batch, train, opt, neg_ids=batch)
+        if train and not isinstance(optimizer, _opt.SGD):
+            d.optimizer = _hip.OPT_GRAD
+            for i in range(4):
+                d.grad_out[i] = 16
         if int(lib.kge_step_workspace_bytes(d)) == 0:
             cache[key] = "kge_step: " + lib.kge_last_error().decode(errors="replace")
         else:
@@ -277,14 +287,16 @@ class FusedStep:
             need = int(self.lib.kge_step_workspace_bytes(d))
             if need == 0:   # invalid descriptor: kge_step re-validates and reports the status
                 _hip.check(self.lib.kge_step(d, _hip.stream_handle(self.device)), "kge_step")
+            sig = int(self.lib.kge_step_plan_signature(d))
             if self.workspace.numel() < need:
                 # zero-filled once: the step's tickets / destination counters
                 # live in the workspace and reset themselves between calls
                 self.workspace = torch.zeros(need, dtype=torch.uint8, device=self.device)
-            elif cached is not None:
-                # a different plan lays the workspace out differently: its
-                # counters must start from zeros again
+            elif sig != getattr(self, "_ws_sig", None):
+                # a different plan lays the workspace out differently (the
+                # library would refuse the stamped buffer): zeros again
                 self.workspace.zero_()
+            self._ws_sig = sig
             d.workspace = self.workspace.data_ptr()
             d.workspace_bytes = self.workspace.numel()
             self._cache = (key, d)

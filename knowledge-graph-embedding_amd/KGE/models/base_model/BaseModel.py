@@ -40,6 +40,24 @@ def _world_size():
     return d.get_world_size() if d.is_available() and d.is_initialized() else 1
 
 
+def _is_rank0():
+    d = torch.distributed
+    return not (d.is_available() and d.is_initialized()) or d.get_rank() == 0
+
+
+def _shared_seed(seed):
+    """Multi-GPU: every rank must shuffle the same global stream (each scores
+    its slice of the same global batch, ``_run_single_batch``); with
+    ``seed=None`` rank 0's draw is broadcast so the ranks agree."""
+    if seed is not None or _world_size() == 1:
+        return seed
+    d = torch.distributed
+    dev = engine.device() if d.get_backend() == "nccl" else torch.device("cpu")
+    s = torch.tensor([int.from_bytes(os.urandom(7), "little")], dtype=torch.int64, device=dev)
+    d.broadcast(s, src=0)
+    return int(s.item())
+
+
 class KGEModel:
     """Base class for KGE models (``BaseModel.py:23-56``)."""
 
@@ -119,6 +137,7 @@ class KGEModel:
     def _prepare_for_train(self, train_X, val_X):
         """``BaseModel.py:192-278``: batch counts, iterators, init, optimizer, sampler."""
         self._device = engine.device()
+        self.seed = _shared_seed(self.seed)
         n_train = calculate_data_size(train_X)
         self._batch_count_train = int(np.ceil(n_train / self.batch_size))
         train_iter = set_tf_iterator(train_X, self.batch_size, shuffle=True, buffer_size=n_train,
@@ -162,8 +181,8 @@ class KGEModel:
     def _run_single_batch(self, batch_data, is_train):
         """One batch (``BaseModel.py:293-330``); returns the loss as a device scalar."""
         opt = self._optimizer if is_train else None
-        reason = engine.fused_plan(self, opt)
         world = _world_size()
+        reason = engine.fused_plan(self, opt, batch_data.shape[0] // world)
         if reason is None:
             if self._fused is None:
                 if world > 1:
@@ -287,44 +306,75 @@ class KGEModel:
 
     # ------------------------------------------------------------ logging / ckpt
     def _log_scalar(self, split, value, step):
+        if not _is_rank0():
+            return
         path = os.path.join(self.log_path, "scalar", split)
         os.makedirs(path, exist_ok=True)
         with open(os.path.join(path, "loss.jsonl"), "a") as f:
             f.write(json.dumps({"step": step, "loss": value}) + "\n")
 
-    def _log_embeddings_histogram(self, step, bucket_count=30):
+    def _log_embeddings_histogram(self, step, bucket_count=30, chunk=1 << 24):
         """``tf.summary.histogram`` of every weight each epoch (``BaseModel.py:162,470-483``),
         written as JSON lines ``log_path/histogram/<name>.jsonl`` (TensorBoard is not installed):
         TensorBoard's bucketing in float64 -- ``bucket_count`` equal-width buckets from min to max
         (a value at max in the last one), or one bucket ``[x - 0.5, x + 0.5]`` when every value is
-        ``x``; ``[left, right, count]`` per bucket. Computed on the weights' device."""
-        self.sync_weights()   # multi-GPU: the shards are the authoritative entity rows
+        ``x``; ``[left, right, count]`` per bucket. Computed on the weights' device, ``chunk``
+        values at a time (float64 only per chunk: a 50M-row table is never copied whole). With
+        row-sharded entity tables (multi-GPU sparse mode) each rank counts its own shard and the
+        min / max / counts are all-reduced; rank 0 writes the file."""
+        d = torch.distributed
+        dist_on = d.is_available() and d.is_initialized()
+        rank0 = not dist_on or d.get_rank() == 0
+        parts = {}
+        if self._fused is not None and hasattr(self._fused, "entity_parts"):
+            parts = self._fused.entity_parts()     # {name: this rank's rows} (sparse mode only)
         path = os.path.join(self.log_path, "histogram")
-        os.makedirs(path, exist_ok=True)
+        if rank0:
+            os.makedirs(path, exist_ok=True)
         for name, w in self.model_weights.items():
-            x = w.detach().reshape(-1).to(torch.float64)
-            if x.numel() == 0:
+            sharded = name in parts
+            x = (parts[name] if sharded else w.detach()).reshape(-1)
+            n = torch.tensor([x.numel()], dtype=torch.float64, device=x.device)
+            lo = torch.tensor([np.inf], dtype=torch.float64, device=x.device)
+            hi = torch.tensor([-np.inf], dtype=torch.float64, device=x.device)
+            for c0 in range(0, x.numel(), chunk):
+                a, b = torch.aminmax(x[c0:c0 + chunk])
+                lo = torch.minimum(lo, a.to(torch.float64))
+                hi = torch.maximum(hi, b.to(torch.float64))
+            if sharded:
+                d.all_reduce(n)
+                d.all_reduce(lo, op=d.ReduceOp.MIN)
+                d.all_reduce(hi, op=d.ReduceOp.MAX)
+            total, lo, hi = float(n), float(lo), float(hi)
+            if total == 0:
                 buckets = []
+            elif lo == hi:
+                buckets = [[lo - 0.5, hi + 0.5, total]]
             else:
-                lo, hi = torch.aminmax(x)
-                lo, hi = float(lo), float(hi)
-                if lo == hi:
-                    buckets = [[lo - 0.5, hi + 0.5, float(x.numel())]]
-                else:
-                    width = (hi - lo) / bucket_count
-                    idx = torch.clamp(torch.floor((x - lo) / width).to(torch.int64), max=bucket_count - 1)
-                    counts = torch.bincount(idx, minlength=bucket_count).to(torch.float64).cpu().tolist()
-                    edges = np.linspace(lo, hi, bucket_count + 1)
-                    buckets = [[float(edges[k]), float(edges[k + 1]), counts[k]] for k in range(bucket_count)]
-            with open(os.path.join(path, "%s.jsonl" % name), "a") as f:
-                f.write(json.dumps({"step": step, "buckets": buckets}) + "\n")
+                width = (hi - lo) / bucket_count
+                counts = torch.zeros(bucket_count, dtype=torch.float64, device=x.device)
+                for c0 in range(0, x.numel(), chunk):
+                    xc = x[c0:c0 + chunk].to(torch.float64)
+                    idx = torch.clamp(torch.floor((xc - lo) / width).to(torch.int64), max=bucket_count - 1)
+                    counts += torch.bincount(idx, minlength=bucket_count).to(torch.float64)
+                if sharded:
+                    d.all_reduce(counts)
+                counts = counts.cpu().tolist()
+                edges = np.linspace(lo, hi, bucket_count + 1)
+                buckets = [[float(edges[k]), float(edges[k + 1]), counts[k]] for k in range(bucket_count)]
+            if rank0:
+                with open(os.path.join(path, "%s.jsonl" % name), "a") as f:
+                    f.write(json.dumps({"step": step, "buckets": buckets}) + "\n")
 
     def _save_checkpoint(self):
         """``CheckpointManager(max_to_keep=1).save()`` (``BaseModel.py:248-253``)."""
         os.makedirs(self.log_path, exist_ok=True)
         path = os.path.join(self.log_path, "ckpt.pt")
-        self.sync_weights()   # multi-GPU: the shards are the authoritative entity rows
-        torch.save({k: v.detach().cpu() for k, v in self.model_weights.items()}, path)
+        self.sync_weights()   # multi-GPU: the shards are the authoritative entity rows (collective)
+        if _is_rank0():
+            torch.save({k: v.detach().cpu() for k, v in self.model_weights.items()}, path)
+        if _world_size() > 1:
+            torch.distributed.barrier()   # the file exists before any rank may restore it
         return path
 
     def _restore_checkpoint(self):

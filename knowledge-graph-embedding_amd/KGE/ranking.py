@@ -176,15 +176,42 @@ def _builders():
             DistMult: _q_distmult, RESCAL: _q_rescal}
 
 
+RANK_Q = 8                  # csrc/kge_step.h kRankQ: queries per count workgroup
+RANK_LDS_BYTES = 64 * 1024  # kge_rank's limit on the staged query rows
+
+
+def query_width(model):
+    """Floats per query row kge_rank stages (its rows in the model's op order)."""
+    from .models.semantic_based.RESCAL import RESCAL
+    from .models.translating_based.RotatE import RotatE
+    w = model.model_weights
+    if isinstance(model, RotatE):
+        return 2 * int(w["rel_emb"].shape[1])
+    if isinstance(model, RESCAL):
+        return int(w["ent_emb"].shape[1])
+    rel = w.get("rel_emb", w.get("rel_inter"))
+    return int(rel.shape[1])
+
+
 def supported(model):
-    """The model class and score function have a batched ranking path."""
+    """The model class and score function have a batched ranking path that
+    ``kge_rank`` accepts (the same limits it checks: staged query rows within
+    its LDS budget, no complex Dot score) -- otherwise ``evaluate`` keeps the
+    reference's per-triple ``get_rank`` loop."""
     b = _builders().get(type(model))
     if b is None:
         return False
-    if hasattr(model, "score_fn") and _score.fused_descriptor(model.score_fn) is None:
-        return False
+    if hasattr(model, "score_fn"):
+        sd = _score.fused_descriptor(model.score_fn)
+        if sd is None:
+            return False
+        from .models.translating_based.RotatE import RotatE
+        if isinstance(model, RotatE) and sd[0] == _score.SCORE_DOT:
+            return False
     ent = model.model_weights.get("ent_emb") if getattr(model, "model_weights", None) else None
-    return ent is not None and ent.is_cuda
+    if ent is None or not ent.is_cuda:
+        return False
+    return 3 * RANK_Q * ((query_width(model) + 3) & ~3) * 4 <= RANK_LDS_BYTES
 
 
 # ---------------------------------------------------------------- filter
@@ -195,10 +222,19 @@ def filter_index(X, positive_X, side, E):
     removed (tensor_scatter_nd_update writes -inf once per entity)."""
     keep, corrupt = (2, 0) if side == "h" else (0, 2)
     P = positive_X.to(torch.int64)
-    key = P[:, 1] * E + P[:, keep]
-    comb = torch.unique(key * E + P[:, corrupt])          # sorted (key, entity) pairs
-    keys = torch.div(comb, E, rounding_mode="floor")
-    ents = comb - keys * E
+    key = P[:, 1] * E + P[:, keep]            # < R * E: fits int64 for any table
+    ent = P[:, corrupt]
+    # (key, entity) pairs sorted lexicographically by two stable sorts (a
+    # combined key * E + entity overflows int64 once R * E^2 > 2^63), then
+    # de-duplicated
+    o = torch.argsort(ent, stable=True)
+    key, ent = key[o], ent[o]
+    o = torch.argsort(key, stable=True)
+    key, ent = key[o], ent[o]
+    first = torch.ones_like(key, dtype=torch.bool)
+    if key.numel() > 1:
+        first[1:] = (key[1:] != key[:-1]) | (ent[1:] != ent[:-1])
+    keys, ents = key[first], ent[first]
     qk = X[:, 1].to(torch.int64) * E + X[:, keep].to(torch.int64)
     beg = torch.searchsorted(keys, qk, right=False)
     end = torch.searchsorted(keys, qk, right=True)

@@ -492,6 +492,16 @@ class ShardedStep:
             if self.ca:
                 w[self.names["ent_aux"]].copy_(nat[:, self.ce:].reshape(self.aux_shape))
 
+    def entity_parts(self):
+        """Sparse mode: {weight name: this rank's owned entity rows} (histograms
+        reduce over the shards instead of gathering the table). Dense: {}."""
+        if self.mode == "dense":
+            return {}
+        out = {self.names["ent"]: self.shard[:self.valid, :self.ce]}
+        if self.ca:
+            out[self.names["ent_aux"]] = self.shard[:self.valid, self.ce:]
+        return out
+
     def load(self, weights):
         """Write ``weights`` (id order) into this rank's shard and the
         replicated tables (checkpoint restore)."""

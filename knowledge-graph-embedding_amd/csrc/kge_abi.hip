@@ -52,6 +52,7 @@ struct Plan {
   int hbits;
   uint64_t o_gnegp, o_gpos2, o_gdense[3], o_dpart;   // TransH / TransD
   bool rescal, transr, proj, td, pj_dense;
+  uint32_t sig;   // workspace plan signature
 };
 
 int score_sk(int kind, float p) {
@@ -162,8 +163,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     return fail(KGE_EINVAL, "sampler idx_dtype must match triples");
 
   Plan& P = *pl;
+  P = Plan{};   // every offset defined (the signature hashes them)
   StepArgs& A = P.A;
-  A = StepArgs{};
   const int K = d->negative_ratio;
   const int Kside = d->corrupt_side == KGE_SIDE_HT ? K / 2 : K;
   const int Keff = d->corrupt_side == KGE_SIDE_HT ? 2 * Kside : K;
@@ -386,6 +387,22 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     }
   }
   P.ws_bytes = std::max<uint64_t>(off, 256);
+  // the plan's workspace signature (kge_hip.h): FNV-1a over everything that
+  // decides where a counter, list or ticket lives and what it means
+  {
+    const int64_t f[] = {model, B, Keff, Kside, d->corrupt_side, E, R, entc, relc, rowlen, d->dim, d->dim_rel,
+                         (int64_t)compact, cap, hbits, kshift, nWG, P.G.gridU, vec, ncp, wpp, SW, d->optimizer,
+                         d->flags, d->constraint, d->shard_count, (int64_t)P.ws_bytes,
+                         (int64_t)P.o_cnt, (int64_t)P.o_htab, (int64_t)P.o_coef, (int64_t)P.o_snap,
+                         (int64_t)P.o_gpos, (int64_t)P.o_part, (int64_t)P.o_list, (int64_t)P.o_ovf,
+                         (int64_t)P.o_upart, (int64_t)P.o_leaders, (int64_t)P.o_sorted, (int64_t)P.o_relseg,
+                         (int64_t)P.o_gneg, (int64_t)P.o_dpart};
+    uint32_t h = 2166136261u;
+    for (const int64_t v : f)
+      for (int b = 0; b < 8; ++b) h = (h ^ (uint32_t)((uint64_t)v >> (8 * b) & 0xFF)) * 16777619u;
+    P.sig = h ? h : 1u;
+    A.sig = P.sig;
+  }
   return KGE_OK;
 }
 
@@ -409,34 +426,7 @@ __global__ __launch_bounds__(256) void sample_kernel(SamplerView s, const void* 
   if (err) set_status(status, err);
 }
 
-// ------------------------------------------------------------ apply kernels
-// var += -lr * clip * g  (SGD) ; keras Adam over every element (ADAM).
-__global__ __launch_bounds__(256) void apply_kernel(float* __restrict__ w, int64_t rows, int32_t cols, int64_t ld,
-                                                     const float* __restrict__ g, const float* __restrict__ norm2,
-                                                     float lr, float clip, int adam, float* __restrict__ m,
-                                                     float* __restrict__ v, float b1, float b2, float eps,
-                                                     float lr_t) {
-  const float n = sqrtf(*norm2);
-  const float cs = clip / fmaxf(n, clip);
-  const int64_t total = rows * (int64_t)cols;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total;
-       q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = q / cols;
-    const int c = (int)(q - r * cols);
-    const float gv = g[q] * cs;
-    float* wp = w + r * ld + c;
-    if (!adam) {
-      *wp = *wp + gv * (-lr);
-    } else {
-      const float mv = b1 * m[q] + (1.f - b1) * gv;
-      const float vv = b2 * v[q] + (1.f - b2) * (gv * gv);
-      m[q] = mv;
-      v[q] = vv;
-      *wp = *wp - lr_t * mv / (sqrtf(vv) + eps);
-    }
-  }
-}
-
+// ------------------------------------------------------------ apply rows
 // rows[i] of var += -lr * clip * g[i]: one wave per listed row
 __global__ __launch_bounds__(256) void apply_rows_kernel(float* __restrict__ w, int64_t ld, int32_t cols,
                                                           const int64_t* __restrict__ rows, int64_t n,
@@ -486,12 +476,12 @@ kge_status kge_apply(const kge_apply_desc* d, void* stream) {
     const double t = (double)d->iteration;
     lr_t = (double)d->lr * std::sqrt(1.0 - std::pow((double)d->beta_2, t)) / (1.0 - std::pow((double)d->beta_1, t));
   }
-  const int64_t total = t.rows * t.cols;
-  if (total == 0) return KGE_OK;
-  const int64_t blocks = std::min<int64_t>(ceil_div(total, 256), 8192);
-  hipLaunchKernelGGL(apply_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, t.data, t.rows,
-                     (int32_t)t.cols, t.ld, d->grad, d->norm2, d->lr, d->clip_norm, adam ? 1 : 0, d->m, d->v,
-                     d->beta_1, d->beta_2, d->epsilon, (float)lr_t);
+  ApplyArgs a{};
+  a.w = t.data; a.rows = t.rows; a.cols = (int32_t)t.cols; a.ld = t.ld;
+  a.g = d->grad; a.norm2 = d->norm2; a.lr = d->lr; a.clip = d->clip_norm;
+  a.adam = adam ? 1 : 0; a.m = d->m; a.v = d->v;
+  a.b1 = d->beta_1; a.b2 = d->beta_2; a.eps = d->epsilon; a.lr_t = (float)lr_t;
+  launch_apply(a, (hipStream_t)stream);
   return hip_check("kge_apply");
 }
 
@@ -521,6 +511,12 @@ uint64_t kge_step_workspace_bytes(const kge_step_desc* d) {
   Plan P;
   if (make_plan(d, &P) != KGE_OK) return 0;
   return P.ws_bytes;
+}
+
+uint32_t kge_step_plan_signature(const kge_step_desc* d) {
+  Plan P;
+  if (make_plan(d, &P) != KGE_OK) return 0;
+  return P.sig;
 }
 
 kge_status kge_step(const kge_step_desc* d, void* stream) {
@@ -598,6 +594,8 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     RA.ctl = A.ctl;
     RA.norm2_out = A.norm2_out;
     RA.status = A.status;
+    RA.sig = A.sig;
+    RA.loss_out = A.loss_out;
   }
 
   PjPlan J{};
@@ -651,7 +649,8 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     for (int v = 0; v < (P.td ? 2 : 1); ++v) {
       const int64_t blocks = std::min<int64_t>(ceil_div(tabs[v]->rows, kWaves), 4096);
       hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, tabs[v]->data,
-                         tabs[v]->rows, (int32_t)tabs[v]->cols, tabs[v]->ld, P.td ? 1 : 0, 1.0f);
+                         tabs[v]->rows, (int32_t)tabs[v]->cols, tabs[v]->ld, P.td ? 1 : 0, 1.0f, A.ctl, A.sig,
+                         A.status);
     }
   }
   if (P.transr && d->constraint && !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT)) {
@@ -660,7 +659,7 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     for (int v = 0; v < 2; ++v) {
       const int64_t blocks = std::min<int64_t>(ceil_div(tabs[v]->rows, kWaves), 4096);
       hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, tabs[v]->data,
-                         tabs[v]->rows, (int32_t)tabs[v]->cols, tabs[v]->ld, 1, 1.0f);
+                         tabs[v]->rows, (int32_t)tabs[v]->cols, tabs[v]->ld, 1, 1.0f, A.ctl, A.sig, A.status);
     }
   }
   // _constraint_loss assigns before scoring (BaseModel.py:319): fused into
@@ -670,7 +669,7 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   if (renorm && !(A.fuse_norm && d->batch > 0)) {
     const int64_t blocks = std::min<int64_t>(ceil_div(d->ent.rows, kWaves), 4096);
     hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, d->ent.data,
-                       d->ent.rows, (int32_t)d->ent.cols, d->ent.ld, 0, 1.0f);
+                       d->ent.rows, (int32_t)d->ent.cols, d->ent.ld, 0, 1.0f, A.ctl, A.sig, A.status);
   }
   if (d->batch == 0) {
     (void)hipMemsetAsync(d->loss_out, 0, sizeof(float), st);
@@ -691,10 +690,11 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
       const float* gs[2] = {A.gent, RA.grel};
       for (int v = 0; v < 2; ++v) {
         const kge_table& t = *tabs[v];
-        const int64_t blocks = std::min<int64_t>(ceil_div(t.rows * t.cols, 256), 8192);
-        hipLaunchKernelGGL(apply_kernel, dim3((unsigned)blocks), dim3(256), 0, st, t.data, t.rows, (int32_t)t.cols,
-                           t.ld, gs[v], (const float*)&A.ctl->dn2[v], d->lr, d->clip_norm, 0, (float*)nullptr,
-                           (float*)nullptr, 0.f, 0.f, 0.f, 0.f);
+        ApplyArgs a{};
+        a.w = t.data; a.rows = t.rows; a.cols = (int32_t)t.cols; a.ld = t.ld;
+        a.g = gs[v]; a.norm2 = &A.ctl->dn2[v]; a.lr = d->lr; a.clip = d->clip_norm;
+        a.ctl = A.ctl; a.sig = A.sig; a.status = A.status;
+        launch_apply(a, st);
       }
     }
   } else {
@@ -797,7 +797,8 @@ kge_status kge_constrain_rows(kge_table t, int32_t kind, float value, void* stre
   if (t.rows == 0) return KGE_OK;
   const int64_t blocks = std::min<int64_t>(ceil_div(t.rows, kWaves), 4096);
   hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, t.data,
-                     t.rows, (int32_t)t.cols, t.ld, kind, value);
+                     t.rows, (int32_t)t.cols, t.ld, kind, value, (StepCtl*)nullptr, 0u,
+                     (int32_t*)nullptr);
   return hip_check("kge_constrain_rows");
 }
 

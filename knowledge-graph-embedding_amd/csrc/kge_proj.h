@@ -243,6 +243,7 @@ __device__ __forceinline__ void stash(const Frag<VEC, NC>& f, float* img) {
 
 template <bool TD, int VEC, int NC, int SK>
 __global__ __launch_bounds__(kPjThreads) void proj_kernel(StepArgs A, PjArgs P) {
+  if (ws_refused(A.ctl, A.sig, A.status, A.loss_out)) return;
   using F = Frag<VEC, NC>;
   constexpr int FL = KGE_WAVE * VEC * NC;
   constexpr int U = NC == 1 ? 4 : 2;                 // slots per batch

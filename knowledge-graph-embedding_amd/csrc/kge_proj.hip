@@ -22,6 +22,7 @@ kge_status launch_proj_transd(const StepArgs& A, const StepGeom& G, const PjArgs
 __global__ __launch_bounds__(256) void transh_dense_kernel(StepArgs A, PjPlan J) {
   __shared__ float s_w[4][4];
   __shared__ int s_last;
+  if (ws_refused(A.ctl, A.sig, A.status, A.loss_out)) return;
   const int lane = lane_id(), wv = wave_id();
   const int64_t E = A.ent.rows, R = A.rel.rows;
   const int d = A.ent.cols;
@@ -126,19 +127,6 @@ __global__ __launch_bounds__(256) void transh_dense_kernel(StepArgs A, PjPlan J)
   }
 }
 
-// clip + SGD of one dense gradient (kge_abi.hip apply_kernel's SGD branch)
-__global__ __launch_bounds__(256) void pj_apply_kernel(float* __restrict__ w, int64_t rows, int32_t cols, int64_t ld,
-                                                       const float* __restrict__ g, const float* __restrict__ norm2,
-                                                       float lr, float clip) {
-  const float cs = clip / fmaxf(sqrtf(*norm2), clip);
-  const int64_t total = rows * (int64_t)cols;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = q / cols;
-    float* wp = w + r * ld + (q - r * cols);
-    *wp = *wp + (g[q] * cs) * (-lr);
-  }
-}
-
 template <int VEC, int NC>
 static void upd_mat(const StepArgs& A, unsigned grid, hipStream_t st) {
   hipLaunchKernelGGL((update_kernel<Materialised, VEC, NC, SK_DOT>), dim3(grid), dim3(kUpdThreads), 0, st, A);
@@ -213,10 +201,11 @@ kge_status launch_step_proj(const StepArgs& A, const StepGeom& G, const PjPlan& 
     if (!A.grad_mode) {
       const TabView tabs[3] = {A.ent, A.rel, J.raux_tab};
       for (int v = 0; v < 3; ++v) {
-        const int64_t total = tabs[v].rows * (int64_t)tabs[v].cols;
-        const unsigned blocks = (unsigned)std::min<int64_t>((total + 255) / 256, 8192);
-        hipLaunchKernelGGL(pj_apply_kernel, dim3(blocks), dim3(256), 0, st, tabs[v].p, tabs[v].rows, tabs[v].cols,
-                           tabs[v].ld, (const float*)J.gdense[v], (const float*)&A.ctl->dn2[v], A.lr, A.clip_norm);
+        ApplyArgs a{};
+        a.w = tabs[v].p; a.rows = tabs[v].rows; a.cols = tabs[v].cols; a.ld = tabs[v].ld;
+        a.g = J.gdense[v]; a.norm2 = &A.ctl->dn2[v]; a.lr = A.lr; a.clip = A.clip_norm;
+        a.ctl = A.ctl; a.sig = A.sig; a.status = A.status;
+        launch_apply(a, st);
         dbg_sync(st, "apply");
       }
     }

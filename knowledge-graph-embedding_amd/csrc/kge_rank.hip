@@ -28,6 +28,8 @@
 // model's own op order: TransE t-side x = h + r; TransH x = P(h) + r with w_r;
 // TransD r_p; TransR the group's pre-projected candidate table; DistMult
 // h * r; RESCAL R^T h / R t; RotatE h o w / w, t.
+#include <algorithm>
+
 #include "kge_step.h"
 
 namespace kge {
@@ -167,9 +169,11 @@ __global__ __launch_bounds__(256) void rank_pos_kernel(RankArgs A) {
 }
 
 template <int MODE, int PJ, int SK>
-__global__ __launch_bounds__(kRankThreads) void rank_count_kernel(RankArgs A, int64_t nchunk) {
+__global__ __launch_bounds__(kRankThreads) void rank_count_kernel(RankArgs A, int64_t g0, int64_t c0) {
   extern __shared__ __attribute__((aligned(16))) float qs[];
-  const int64_t g = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
+  // x: query group (consecutive workgroups share a candidate chunk, so its
+  // rows are reused from L2 across groups), y: candidate chunk
+  const int64_t g = g0 + blockIdx.x, ch = c0 + blockIdx.y;
   const int64_t q0i = g * kRankQ;
   const int nq = (int)min<int64_t>(kRankQ, A.n - q0i);
   const int LQ = (A.dim + 3) & ~3;
@@ -228,8 +232,13 @@ static void rank_launch(const RankArgs& A, hipStream_t st) {
   const int64_t nchunk = (A.E + kRankThreads - 1) / kRankThreads;
   const int64_t ng = (A.n + kRankQ - 1) / kRankQ;
   const size_t lds = (size_t)3 * kRankQ * ((A.dim + 3) & ~3) * 4;
-  hipLaunchKernelGGL((rank_count_kernel<MODE, PJ, SK>), dim3((unsigned)(nchunk * ng)), dim3(kRankThreads), lds, st, A,
-                     nchunk);
+  // grid limits: y <= 65535 chunks, x * 256 work-items < 2^32 per launch
+  constexpr int64_t kMaxY = 65535, kMaxX = (int64_t)1 << 22;
+  for (int64_t c0 = 0; c0 < nchunk; c0 += kMaxY)
+    for (int64_t g0 = 0; g0 < ng; g0 += kMaxX)
+      hipLaunchKernelGGL((rank_count_kernel<MODE, PJ, SK>),
+                         dim3((unsigned)std::min(ng - g0, kMaxX), (unsigned)std::min(nchunk - c0, kMaxY)),
+                         dim3(kRankThreads), lds, st, A, g0, c0);
   hipLaunchKernelGGL((rank_filter_kernel<MODE, PJ, SK>), dim3((unsigned)((A.n + 3) / 4)), dim3(256), 0, st, A);
 }
 

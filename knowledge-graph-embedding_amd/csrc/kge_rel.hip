@@ -223,6 +223,7 @@ __global__ __launch_bounds__(256) void rel_pair_kernel(RelArgs P) {
 // gradient and reduces its norm^2 (last workgroup, fixed order).
 __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  if (ws_refused(P.ctl, P.sig, P.status, P.loss_out)) return;
   const int d = P.d, nct = (d + 15) / 16, D16 = nct * 16;
   const int64_t r = blockIdx.x / nct;
   const int ti = (int)(blockIdx.x % nct), i0 = ti * 16;
@@ -347,6 +348,7 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
 }
 
 __global__ __launch_bounds__(256) void rel_dr_norm_kernel(RelArgs P, int n) {
+  if (ws_refused(P.ctl, P.sig, P.status, P.loss_out)) return;
   __shared__ float s_n2[4], s_m2[4];
   const int lane = lane_id(), wv = wave_id();
   float s = 0.f, m = 0.f;
@@ -386,7 +388,9 @@ __device__ __forceinline__ float chunk_sq(const float* x, int64_t c0, int cols, 
 }
 
 __global__ __launch_bounds__(256) void reg_loss_kernel(TabView ent, TabView rel, float lam, float* part,
-                                                        StepCtl* ctl, float* loss_out, float* loss_accum) {
+                                                        StepCtl* ctl, float* loss_out, float* loss_accum,
+                                                        uint32_t sig, int32_t* status) {
+  if (ws_refused(ctl, sig, status, loss_out)) return;
   __shared__ float s_p[4][2];
   __shared__ int s_last;
   const int lane = lane_id(), wv = wave_id();
@@ -475,9 +479,9 @@ void launch_rel_post(const RelArgs& P, hipStream_t st) {
   hipLaunchKernelGGL(rel_dr_norm_kernel, dim3(1), dim3(256), 0, st, P, (int)(P.rel.rows * nct));
 }
 void launch_reg_loss(const TabView& ent, const TabView& rel, float lam, float* part, StepCtl* ctl,
-                     float* loss_out, float* loss_accum, hipStream_t st) {
+                     float* loss_out, float* loss_accum, uint32_t sig, int32_t* status, hipStream_t st) {
   hipLaunchKernelGGL(reg_loss_kernel, dim3(kRegWGs), dim3(256), 0, st, ent, rel, lam, part, ctl, loss_out,
-                     loss_accum);
+                     loss_accum, sig, status);
 }
 
 }  // namespace kge

@@ -39,8 +39,47 @@ struct StepCtl {
   uint32_t reg_ticket;     // regulariser-loss workgroups done
   float dn2[4];            // norm^2 of the dense (duplicate-summed) gradient per variable
   float reg_r2;            // RESCAL train step: sum_r ||R_r||_F^2 (rel_dr partials)
-  uint32_t pad1[2];
+  uint32_t plan_sig;       // signature of the plan that last used the workspace (0: fresh)
+  uint32_t pad1;
 };
+
+// Workspace plan guard (include/kge_hip.h, "workspace"). Every kernel of a
+// step that writes a table or a caller-visible output calls this first. A
+// fresh (zero-filled) workspace is claimed by the first guarded kernel; one
+// last used by a different plan -- its counters and lists laid out for other
+// sizes -- is refused by every guarded kernel of the step, so nothing is
+// written: the status word gets KGE_EWORKSPACE and the loss NaN. The value
+// only ever goes 0 -> sig, so every workgroup of every kernel of a step takes
+// the same decision. The word is read with a plain uniform load at kernel
+// entry (a scalar load: a launch of 10^5 waves must not queue 10^5 requests on
+// the one L2 channel that holds it -- an atomic load there cost C2-50M's
+// update kernel 120 us); it is written only with a vector store.
+__device__ __forceinline__ bool ws_refused(StepCtl* ctl, uint32_t sig, int32_t* status, float* loss_out) {
+  const uint32_t s = *reinterpret_cast<const uint32_t*>(&ctl->plan_sig);
+  const bool lead = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
+  if (s == 0u || s == sig) {
+    if (s == 0u && lead) __hip_atomic_store(&ctl->plan_sig, sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
+  if (lead) {
+    set_status(status, KGE_EWORKSPACE);
+    if (loss_out) loss_out[0] = __builtin_nanf("");
+  }
+  return true;
+}
+
+// Optimizer apply over a whole table (kge_apply, and the dense-gradient
+// steps' in-step SGD): clip_by_norm with the variable's norm^2, then SGD or
+// keras Adam (kge_hip.h kge_apply_desc). Guarded when launched by a step
+// (ctl != nullptr).
+struct ApplyArgs {
+  float* w; int64_t rows; int32_t cols; int64_t ld;
+  const float* g; const float* norm2;
+  float lr, clip;
+  int adam; float* m; float* v; float b1, b2, eps, lr_t;
+  StepCtl* ctl; uint32_t sig; int32_t* status;
+};
+void launch_apply(const ApplyArgs& a, hipStream_t st);
 
 // Everything a step kernel needs, passed by value (kernarg segment).
 struct StepArgs {
@@ -139,6 +178,7 @@ struct StepArgs {
   float* neg_score_out;
   float* norm2_out;
   int32_t* status;
+  uint32_t sig;     // plan signature (ws_refused)
 };
 
 struct StepGeom {
@@ -175,13 +215,15 @@ struct RelArgs {
   StepCtl* ctl;
   float* norm2_out;
   int32_t* status;
+  uint32_t sig;              // plan signature (ws_refused)
+  float* loss_out;
 };
 void launch_rel_rank(const RelArgs& R, hipStream_t st);
 void launch_rel_ctx(const RelArgs& R, hipStream_t st);      // u, v
 void launch_rel_post(const RelArgs& R, hipStream_t st);     // g_h, g_t, dR (+ dense term, norm^2)
 // lambda * (mean_e ||e||^2 + mean_r ||R_r||_F^2) added to the step loss (RESCAL.py:190-198)
 void launch_reg_loss(const TabView& ent, const TabView& rel, float lam, float* part, StepCtl* ctl,
-                     float* loss_out, float* loss_accum, hipStream_t st);
+                     float* loss_out, float* loss_accum, uint32_t sig, int32_t* status, hipStream_t st);
 constexpr int kRegWGs = 1024;   // regulariser sweep workgroups (256-float chunks dealt round-robin)
 
 // first sorted position in [lo, hi) whose relation is >= r (srel ascending)
@@ -268,7 +310,7 @@ void launch_stream(const void* tri, bool i64, int64_t n, int64_t start, int64_t 
                    void* out, hipStream_t st);
 
 __global__ void constrain_rows_kernel(float* t, int64_t rows, int32_t cols, int64_t ld, int kind,
-                                      float value);
+                                      float value, StepCtl* ctl, uint32_t sig, int32_t* status);
 
 // Byte offsets of the score kernel's dynamic LDS carve (shared by host and
 // device so the launch size always matches the kernel's view).

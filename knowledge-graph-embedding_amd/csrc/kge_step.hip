@@ -26,6 +26,8 @@
 //                   positives' own row gradients added, clip scale and SGD
 //                   (BaseModel.py:328, keras SGD ResourceScatterAdd) applied
 //                   with ONE read-modify-write per touched row.
+#include <algorithm>
+
 #include "kge_proj.h"
 
 namespace kge {
@@ -36,7 +38,9 @@ namespace kge {
 // Each wave owns 4 rows and issues all their loads before reducing.
 __global__ __launch_bounds__(256) void constrain_rows_kernel(float* __restrict__ t, int64_t rows,
                                                               int32_t cols, int64_t ld, int kind,
-                                                              float value) {
+                                                              float value, StepCtl* ctl, uint32_t sig,
+                                                              int32_t* status) {
+  if (ctl && ws_refused(ctl, sig, status, nullptr)) return;   // launched by a step: guarded
   constexpr int RPW = 4;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x / KGE_WAVE);
   const bool v4 = (cols % 4 == 0) && (ld % 4 == 0) && (((uintptr_t)t & 15) == 0) && cols <= 4 * KGE_WAVE;
@@ -89,6 +93,76 @@ __global__ __launch_bounds__(256) void constrain_rows_kernel(float* __restrict__
       }
     }
   }
+}
+
+// ------------------------------------------------------------ apply
+// var += -lr * clip(g) (keras SGD) or keras Adam over every element
+// (kge_hip.h kge_apply_desc). A contiguous table (ld == cols) is one flat
+// float4 stream (no per-element row division); a strided one goes a wave per
+// row, float4 lanes when the row allows.
+__device__ __forceinline__ void apply_one(const ApplyArgs& a, float cs, float& w, float g, float& m, float& v) {
+  const float gv = g * cs;
+  if (!a.adam) {
+    w = w + gv * (-a.lr);
+  } else {
+    m = a.b1 * m + (1.f - a.b1) * gv;
+    v = a.b2 * v + (1.f - a.b2) * (gv * gv);
+    w = w - a.lr_t * m / (sqrtf(v) + a.eps);
+  }
+}
+__device__ __forceinline__ void apply4(const ApplyArgs& a, float cs, float* w, const float* g, float* m, float* v) {
+  float4 W = *reinterpret_cast<const float4*>(w);
+  const float4 G = *reinterpret_cast<const float4*>(g);
+  float4 Mv = make_float4(0.f, 0.f, 0.f, 0.f), Vv = Mv;
+  if (a.adam) {
+    Mv = *reinterpret_cast<const float4*>(m);
+    Vv = *reinterpret_cast<const float4*>(v);
+  }
+  apply_one(a, cs, W.x, G.x, Mv.x, Vv.x);
+  apply_one(a, cs, W.y, G.y, Mv.y, Vv.y);
+  apply_one(a, cs, W.z, G.z, Mv.z, Vv.z);
+  apply_one(a, cs, W.w, G.w, Mv.w, Vv.w);
+  *reinterpret_cast<float4*>(w) = W;
+  if (a.adam) {
+    *reinterpret_cast<float4*>(m) = Mv;
+    *reinterpret_cast<float4*>(v) = Vv;
+  }
+}
+
+__global__ __launch_bounds__(256) void apply_kernel(ApplyArgs a, int flat4) {
+  if (a.ctl && ws_refused(a.ctl, a.sig, a.status, nullptr)) return;
+  const float cs = a.clip / fmaxf(sqrtf(*a.norm2), a.clip);
+  float dm = 0.f, dv = 0.f;
+  if (flat4) {
+    const int64_t n4 = a.rows * (int64_t)a.cols / 4;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x)
+      apply4(a, cs, a.w + 4 * q, a.g + 4 * q, a.adam ? a.m + 4 * q : nullptr, a.adam ? a.v + 4 * q : nullptr);
+    return;
+  }
+  const bool v4 = a.cols % 4 == 0 && a.ld % 4 == 0 && ((uintptr_t)a.w % 16) == 0 && ((uintptr_t)a.g % 16) == 0 &&
+                  (!a.adam || (((uintptr_t)a.m % 16) == 0 && ((uintptr_t)a.v % 16) == 0));
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x / KGE_WAVE);
+  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x / KGE_WAVE) + wave_id(); r < a.rows; r += nw) {
+    float* wr = a.w + r * a.ld;
+    const int64_t go = r * (int64_t)a.cols;
+    if (v4) {
+      for (int c = 4 * lane_id(); c < a.cols; c += 4 * KGE_WAVE)
+        apply4(a, cs, wr + c, a.g + go + c, a.adam ? a.m + go + c : nullptr, a.adam ? a.v + go + c : nullptr);
+    } else {
+      for (int c = lane_id(); c < a.cols; c += KGE_WAVE)
+        apply_one(a, cs, wr[c], a.g[go + c], a.adam ? a.m[go + c] : dm, a.adam ? a.v[go + c] : dv);
+    }
+  }
+}
+
+void launch_apply(const ApplyArgs& a, hipStream_t st) {
+  const int64_t total = a.rows * (int64_t)a.cols;
+  if (total == 0) return;
+  const bool flat4 = a.ld == a.cols && total % 4 == 0 && ((uintptr_t)a.w % 16) == 0 && ((uintptr_t)a.g % 16) == 0 &&
+                     (!a.adam || (((uintptr_t)a.m % 16) == 0 && ((uintptr_t)a.v % 16) == 0));
+  const int64_t work = flat4 ? (total / 4 + 255) / 256 : (a.rows + 3) / 4;
+  const unsigned blocks = (unsigned)std::min<int64_t>(std::max<int64_t>(work, 1), 8192);
+  hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, st, a, flat4 ? 1 : 0);
 }
 
 kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int model, int sk,

@@ -39,6 +39,9 @@
 #ifndef KGE_STREAM_ROWS
 #define KGE_STREAM_ROWS 8   // sampled rows per stream batch at NC = 1 (tuning knob)
 #endif
+#ifndef KGE_GUARD_KU
+#define KGE_GUARD_KU 1      // update kernel: workspace plan guard at entry (tuning / A-B knob)
+#endif
 #ifndef KGE_UPDATE_U
 #define KGE_UPDATE_U 8      // update kernel: list entries in flight per wave at NC = 1 (tuning knob)
 #endif
@@ -244,6 +247,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   float* s_misc = reinterpret_cast<float*>(smem + L.misc);
   __shared__ int s_last;
 
+  if (ws_refused(A.ctl, A.sig, A.status, A.loss_out)) return;
   KGE_PROF_INIT();
   const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
   const int grp = wv / wpp, gw = wv % wpp;
@@ -702,6 +706,9 @@ void update_kernel(StepArgs A) {
   __shared__ uint32_t s_scr[kUpdWaves][CHMAX * KGE_WAVE];
   __shared__ uint32_t s_sort[kUpdWaves][kSortMax];    // longer lists: gathered + bitonic-sorted here
 
+#if KGE_GUARD_KU
+  if (ws_refused(A.ctl, A.sig, A.status, A.loss_out)) return;
+#endif
   KGE_PROF_INIT();
   const int lane = lane_id(), wv = wave_id();
   const int64_t E_ = A.ent.rows;

@@ -12,7 +12,9 @@ namespace kge {
 // by rel_dr_norm_kernel (lam = 0: no loss term).
 __global__ __launch_bounds__(256) void partials_norm_kernel(const float* part, int n, StepCtl* ctl, int slot,
                                                             float* norm2_out, float lam, float inv_e, float inv_r,
-                                                            float* loss_out, float* loss_accum) {
+                                                            float* loss_out, float* loss_accum, uint32_t sig,
+                                                            int32_t* status) {
+  if (ws_refused(ctl, sig, status, loss_out)) return;
   __shared__ float s_n2[4], s_e2[4];
   const int lane = lane_id(), wv = wave_id();
   float s = 0.f, e = 0.f;
@@ -46,13 +48,14 @@ static kge_status rescal_vn(const StepArgs& A, const StepGeom& G, const RelArgs&
   launch_score<Rescal, VEC, NC, SK_DOT>(A, G, st);
   // train steps fold the regulariser loss into passes that read every row
   // anyway (rel_dr: each R_r; the dense update: each entity row)
-  if (lam != 0.f && !A.train) launch_reg_loss(A.ent, A.rel, lam, regpart, A.ctl, A.loss_out, A.loss_accum, st);
+  if (lam != 0.f && !A.train) launch_reg_loss(A.ent, A.rel, lam, regpart, A.ctl, A.loss_out, A.loss_accum, A.sig, A.status, st);
   if (ev) (void)hipEventRecord(ev[2], st);
   if (A.train) {
     launch_rel_post(P, st);
     hipLaunchKernelGGL((update_kernel<Rescal, VEC, NC, SK_DOT>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
     hipLaunchKernelGGL(partials_norm_kernel, dim3(1), dim3(256), 0, st, A.upart, (int)G.gridU, A.ctl, 0, A.norm2_out,
-                       lam, 1.f / (float)A.ent.rows, 1.f / (float)A.rel.rows, A.loss_out, A.loss_accum);
+                       lam, 1.f / (float)A.ent.rows, 1.f / (float)A.rel.rows, A.loss_out, A.loss_accum, A.sig,
+                       A.status);
   }
   return KGE_OK;
 }

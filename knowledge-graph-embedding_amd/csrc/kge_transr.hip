@@ -87,6 +87,7 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ float s_w[kTrWaves][4];
   __shared__ int s_last;
+  if (ws_refused(A.ctl, A.sig, A.status, A.loss_out)) return;
   const int d = T.d, k = T.k, K = A.Keff, NR = K + 2, NS = 2 * K + 4;
   const TrLds L = tr_lds(d, k, K);
   const int LX = L.LX, LP = L.LP, D4 = LX - 1, K4 = LP - 1;
@@ -605,6 +606,7 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
 // sorted (positive) order, clip scale, SGD -- or the dense gradient in
 // KGE_OPT_GRAD mode. 1024 elements of M_r per workgroup.
 __global__ __launch_bounds__(256) void transr_proj_apply(StepArgs A, TrArgs T) {
+  if (ws_refused(A.ctl, A.sig, A.status, A.loss_out)) return;
   const int64_t dk = (int64_t)T.d * T.k;
   const int64_t chunks = (dk + 1023) / 1024;
   const int64_t r = blockIdx.x / chunks, ch = blockIdx.x % chunks;

@@ -333,15 +333,23 @@ def _constraint(model, W, L, X, cfg, batch_scale):
 
 def train_step(model, weights, pos, neg_ids, score=("lp", 2.0), loss=("hinge", 1.0), lr=0.01, constraint=True,
                constraint_weight=1.0, side="h+t", train=True, batch_scale=1.0, limit=None,
-               clip_norm=5.0, dtype=F64, optimizer="sgd", adam=(0.9, 0.999, 1e-7)):
+               clip_norm=5.0, dtype=F64, optimizer="sgd", adam=(0.9, 0.999, 1e-7), adam_state=None):
     """One reference step with injected negatives. Returns dict with loss,
     pos_score, neg_score, weights (numpy, updated) and norm2 per variable.
 
     optimizer "sgd": keras SGD (sparse ResourceScatterAdd of -lr * g).
-    optimizer "adam": the FIRST keras Adam step from zero slots (OptimizerV2,
-    TF 2.5): slices de-duplicated (summed per row), m = (1-b1) g,
-    v = (1-b2) g^2, var -= lr_t m / (sqrt(v) + eps) over every row,
-    lr_t = lr sqrt(1-b2) / (1-b1)."""
+    optimizer "adam": keras Adam (OptimizerV2, TF 2.5), BaseModel.py:243-246
+    (the reference's default optimizer), applied at :328. ``adam_state`` =
+    {"t": steps done so far, "slots": {name: (m, v)}} carries the slots and
+    ``optimizer.iterations`` from one call to the next (None: the first step,
+    zero slots); the returned dict holds the advanced state under "adam".
+    Per variable, with t = iterations + 1:
+      sparse (IndexedSlices; _resource_apply_sparse_duplicate_indices sums the
+      duplicates first): m = b1 m over every row, then scatter-add (1-b1) g;
+      v likewise with (1-b2) g^2;
+      dense (ResourceApplyAdam): m += (g - m)(1-b1), v += (g^2 - v)(1-b2);
+      both: var -= lr_t m / (sqrt(v) + eps), lr_t = lr sqrt(1-b2^t) / (1-b1^t),
+      over every row."""
     W = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in weights.items()}
     names = list(W.keys())
     pos = np.asarray(pos, dtype=np.int64)
@@ -360,6 +368,11 @@ def train_step(model, weights, pos, neg_ids, score=("lp", 2.0), loss=("hinge", 1
         lval = loss_fn(loss, ps, ns, batch_scale) + cterm
     out = {"loss": float(lval.detach()), "pos_score": ps.detach().numpy(), "neg_score": ns.detach().numpy(),
            "norm2": {}}
+    if optimizer == "adam" and train:
+        st = adam_state or {"t": 0, "slots": {}}
+        t_adam = st["t"] + 1
+        slots = {k: (torch.as_tensor(np.asarray(m), dtype=dtype).clone(), torch.as_tensor(np.asarray(v), dtype=dtype).clone())
+                 for k, (m, v) in st["slots"].items()}
     if train:
         leaves = [x[2] for x in L.rec]
         grads = torch.autograd.grad(lval, [W[n] for n in names] + leaves, allow_unused=True)
@@ -383,7 +396,7 @@ def train_step(model, weights, pos, neg_ids, score=("lp", 2.0), loss=("hinge", 1
                     out["norm2"][n] = float(l2)
                     tot = tot * clip_norm / max(math.sqrt(float(l2)), clip_norm)
                     if optimizer == "adam":
-                        _adam_first_step(w, tot, lr, *adam)
+                        _adam_step(w, tot, lr, *adam, slots, n, t_adam, dense=True)
                     else:
                         w.add_(-lr * tot)
                 else:
@@ -393,15 +406,26 @@ def train_step(model, weights, pos, neg_ids, score=("lp", 2.0), loss=("hinge", 1
                     out["norm2"][n] = float(l2)
                     vals = vals * clip_norm / max(math.sqrt(float(l2)), clip_norm)
                     if optimizer == "adam":
-                        _adam_first_step(w, torch.zeros_like(w).index_add_(0, idx, vals), lr, *adam)
+                        _adam_step(w, torch.zeros_like(w).index_add_(0, idx, vals), lr, *adam, slots, n, t_adam,
+                                   dense=False)
                     else:
                         w.index_add_(0, idx, -lr * vals)
+        if optimizer == "adam":
+            out["adam"] = {"t": t_adam, "slots": {k: (m.numpy(), v.numpy()) for k, (m, v) in slots.items()}}
     out["weights"] = {k: v.detach().numpy() for k, v in W.items()}
     return out
 
 
-def _adam_first_step(w, g, lr, b1, b2, eps):
-    m = (1 - b1) * g
-    v = (1 - b2) * g * g
-    lr_t = lr * math.sqrt(1 - b2) / (1 - b1)
+def _adam_step(w, g, lr, b1, b2, eps, slots, name, t, dense):
+    """keras Adam on one variable (TF 2.5 OptimizerV2): g is the clipped,
+    duplicate-summed gradient (zero on rows no slice touched)."""
+    m, v = slots.get(name, (torch.zeros_like(w), torch.zeros_like(w)))
+    if dense:      # ResourceApplyAdam
+        m = m + (g - m) * (1 - b1)
+        v = v + (g * g - v) * (1 - b2)
+    else:          # _resource_apply_sparse: decay every row, scatter-add the slices
+        m = m * b1 + (1 - b1) * g
+        v = v * b2 + (1 - b2) * (g * g)
+    slots[name] = (m, v)
+    lr_t = lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
     w.sub_(lr_t * m / (torch.sqrt(v) + eps))

@@ -417,6 +417,58 @@ def test_rotate_k256_cross_wave_merge(hiplib):
     check(ref, got, l_, ps, ns)
 
 
+@pytest.mark.parametrize("B,idx", [(3, torch.int64), (9, torch.int64), (4, torch.int32)])
+def test_rotate_c3_kernel_instance(hiplib, B, idx):
+    """The exact instance the C3 bench times (RotatE.py:126-165): d = 256
+    complex (512-float rows -> two fragment chunks, score_kernel<RotatE, 4, 2,
+    SK_P1, h+t>), K = 256 'h+t' (four waves per positive: the cross-wave
+    online-softmax merge), LpDistance(1), SANS(3, 1) -- vs the oracle; B = 9
+    puts two positives in one workgroup and a partial last workgroup."""
+    from KGE import loss, score
+    ref, got, l_, ps, ns, step, _ = run_case(hiplib, "RotatE", 256, B, 256, "h+t", score.LpDistance(1),
+                                             loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E=700, R=11,
+                                             idx=idx, lr=0.01)
+    check(ref, got, l_, ps, ns)
+
+
+def test_c3_full_size_properties(hiplib):
+    """C3 at its full size (B = 1024, K = 256, d = 256, E = 14,505, R = 237):
+    finite loss and scores <= 0, and a second identical step from the same
+    state reproduces the first bit for bit (destination-major update, no
+    float atomics)."""
+    from KGE import engine, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    dev = _dev()
+    E, R, d, B, K = 14505, 237, 256, 1024, 256
+    g = torch.Generator(device="cpu").manual_seed(3)
+    lim = 5.0 / d
+    ent0 = ((torch.rand(E, d, 2, generator=g) * 2 - 1) * lim).to(dev)
+    rel0 = ((torch.rand(R, d, generator=g) * 2 - 1) * lim).to(dev)
+    pos = torch.stack([torch.randint(0, E, (B,), generator=g), torch.randint(0, R, (B,), generator=g),
+                       torch.randint(0, E, (B,), generator=g)], 1).to(dev)
+    outs = []
+    for _ in range(2):
+        m = _make("RotatE", d, K, "h+t", score.LpDistance(1), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
+                  E, R, UniformStrategy(np.arange(E), seed=8))
+        m.model_weights = {"ent_emb": ent0.clone(), "rel_emb": rel0.clone()}
+        step = engine.FusedStep(m)
+        ps = torch.zeros(B, device=dev)
+        ns = torch.zeros(B * K, device=dev)
+        step(pos, True, optimizers.SGD(0.01), pos_score=ps, neg_score=ns)
+        torch.cuda.synchronize()
+        step.check_status()
+        outs.append((float(step.loss_out.item()), m.model_weights["ent_emb"].clone(),
+                     m.model_weights["rel_emb"].clone(), ps, ns, step.norm2.clone()))
+    loss0 = outs[0][0]
+    assert math.isfinite(loss0) and loss0 > 0
+    assert bool((outs[0][3] <= 0).all()) and bool((outs[0][4] <= 0).all())
+    assert bool(torch.isfinite(outs[0][1]).all()) and bool(torch.isfinite(outs[0][2]).all())
+    assert not torch.equal(outs[0][1], ent0) and not torch.equal(outs[0][2], rel0)
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        assert torch.equal(a, b)
+    assert loss0 == outs[1][0]
+
+
 @pytest.mark.parametrize("model_name", ["TransE", "DistMult", "RotatE", "TransR", "TransH", "TransD"])
 def test_compact_update_large_table(hiplib, model_name):
     """E = 6000 rows vs 8 x (5 + 3) keys: the update kernel visits only the
@@ -556,6 +608,70 @@ def test_consecutive_steps_reuse_workspace(hiplib):
             np.testing.assert_allclose(m.model_weights[k].cpu().numpy(), v, atol=TOL, err_msg="%s step %d" % (k, it))
 
 
+@pytest.mark.parametrize("model_name", ["TransE", "RESCAL", "TransR", "TransH"])
+def test_replan_on_dirty_workspace_is_refused(hiplib, model_name):
+    """kge_hip.h workspace rules: a step whose plan differs from the one
+    stamped in its workspace (a caller that re-plans -- here a new batch size
+    -- without re-zeroing the buffer) is refused on the device: status word
+    KGE_EWORKSPACE, loss NaN, every table unchanged. After a re-zero the same
+    descriptor runs and equals the oracle."""
+    import ctypes
+    from KGE import _hip, engine, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    dev = _dev()
+    rng = np.random.default_rng(51)
+    E, R, d, K = 40, 5, 24, 4
+    k = 20 if model_name == "TransR" else None
+    W = _weights(model_name, E, R, d, rng, k)
+    sc = {"TransE": score.LpDistance(2), "TransR": score.LpDistancePow(2), "TransH": score.LpDistancePow(2)}.get(
+        model_name)
+    sampler = UniformStrategy(np.arange(E), seed=2)
+    m = _make(model_name, d, K, "h+t", sc, loss.SquareErrorLoss(), E, R, sampler, k=k)
+    m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
+    step = engine.FusedStep(m)
+    opt = optimizers.SGD(0.05)
+    posA = np.stack([rng.integers(0, E, 8), rng.integers(0, R, 8), rng.integers(0, E, 8)], 1).astype(np.int64)
+    step(torch.tensor(posA, device=dev), True, opt)      # plan A stamps the workspace
+    torch.cuda.synchronize()
+    step.check_status()
+    before = {kk: v.clone() for kk, v in m.model_weights.items()}
+    posB = np.stack([rng.integers(0, E, 13), rng.integers(0, R, 13), rng.integers(0, E, 13)], 1).astype(np.int64)
+    bB = torch.tensor(posB, device=dev)
+    plane = sampler.offset
+    d_ = step.describe(bB, True, opt)        # draws planes (plane, plane + 1)
+    lib = _hip.lib()
+    sigA = step._ws_sig
+    assert lib.kge_step_plan_signature(d_) not in (0, sigA)
+    need = int(lib.kge_step_workspace_bytes(d_))
+    if step.workspace.numel() < need:     # grow, keeping the stamped head
+        ws = torch.zeros(need, dtype=torch.uint8, device=dev)
+        ws[:step.workspace.numel()] = step.workspace
+        step.workspace = ws
+    d_.workspace = step.workspace.data_ptr()
+    d_.workspace_bytes = step.workspace.numel()
+    assert lib.kge_step(ctypes.byref(d_), _hip.stream_handle(dev)) == _hip.KGE_OK   # host validation passes
+    torch.cuda.synchronize()
+    assert int(step.status.item()) == _hip.KGE_EWORKSPACE
+    with pytest.raises(RuntimeError, match="refused"):
+        step.check_status()
+    assert math.isnan(float(step.loss_out.item()))
+    for kk, v in m.model_weights.items():
+        assert torch.equal(v, before[kk]), kk
+    # re-zeroed: the same plan B runs (same draws as the refused call) and equals the oracle
+    step.workspace.zero_()
+    d_.sampler.offset = plane
+    assert lib.kge_step(ctypes.byref(d_), _hip.stream_handle(dev)) == _hip.KGE_OK
+    torch.cuda.synchronize()
+    step.check_status()
+    neg = orc.negatives(posB, K, "h+t", E, seed=2, plane=plane)
+    Wb = {kk: v.cpu().numpy() for kk, v in before.items()}
+    ref = orc.train_step(model_name, Wb, posB, neg, score=_spec_score(sc) if sc is not None else ("dot", 0.0),
+                         loss=("sqerr",), lr=0.05, constraint_weight=getattr(m, "constraint_weight", 1.0))
+    assert abs(float(step.loss_out.item()) - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"]))
+    for kk, v in ref["weights"].items():
+        np.testing.assert_allclose(m.model_weights[kk].cpu().numpy(), v, atol=TOL, err_msg=kk)
+
+
 def test_hinge_zero_negatives_is_nan(hiplib):
     from KGE import loss, score
     ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransE", 16, 5, 1, "h+t", score.LpDistance(2),
@@ -638,6 +754,54 @@ def test_fused_adam_first_step(hiplib, model_name):
     ref, got, l_, ps, ns, _, _ = run_case(hiplib, model_name, 32, 12, 6, "h+t", sc,
                                           loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), opt="adam", lr=0.01)
     check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("model_name,constraint", [("TransE", True), ("TransE", False), ("RESCAL", True),
+                                                   ("TransH", True), ("DistMult", True), ("TransR", True)])
+def test_fused_adam_three_steps(hiplib, model_name, constraint):
+    """keras Adam past its first step (BaseModel.py:243-246, applied at :328):
+    three consecutive steps through one FusedStep and one Adam optimizer --
+    the m / v slots decay on every row (sparse variables: TransE / DistMult /
+    TransR) or follow ResourceApplyAdam (dense variables: RESCAL's and
+    TransH's full-table regularisers) and lr_t = lr sqrt(1-b2^t)/(1-b1^t) at
+    t = 1, 2, 3 -- against the oracle carrying its own slots."""
+    from KGE import engine, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    dev = _dev()
+    rng = np.random.default_rng(29)
+    E, R, d, B, K = 45, 4, 24, 11, 6
+    k = 20 if model_name == "TransR" else None
+    W = _weights(model_name, E, R, d, rng, k)
+    sc = {"TransE": score.LpDistance(2), "TransH": score.LpDistancePow(2), "TransR": score.LpDistancePow(2)}.get(
+        model_name)
+    lf = loss.SquareErrorLoss() if model_name == "RESCAL" else loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0)
+    sampler = UniformStrategy(np.arange(E), seed=12)
+    m = _make(model_name, d, K, "h+t", sc, lf, E, R, sampler, constraint=constraint, k=k)
+    m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
+    step = engine.FusedStep(m)
+    opt = optimizers.Adam(0.01)
+    ref_w, state = W, None
+    for it in range(3):
+        pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+        plane = sampler.offset
+        step(torch.tensor(pos, device=dev), True, opt)
+        torch.cuda.synchronize()
+        step.check_status()
+        assert opt.iterations == it + 1
+        neg = orc.negatives(pos, K, "h+t", E, seed=12, plane=plane)
+        ref = orc.train_step(model_name, ref_w, pos, neg, score=_spec_score(sc) if sc is not None else ("dot", 0.0),
+                             loss=_spec_loss(lf), lr=0.01, constraint=constraint, optimizer="adam",
+                             adam_state=state, constraint_weight=getattr(m, "constraint_weight", 1.0))
+        ref_w, state = ref["weights"], ref["adam"]
+        assert state["t"] == it + 1
+        assert abs(float(step.loss_out.item()) - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"])), it
+        for kk, v in ref_w.items():
+            np.testing.assert_allclose(m.model_weights[kk].cpu().numpy(), v, atol=TOL,
+                                       err_msg="%s step %d" % (kk, it + 1))
+        for kk, (ms, vs) in state["slots"].items():
+            got = opt.slots[kk]
+            np.testing.assert_allclose(got["m"].cpu().numpy(), ms, atol=TOL, err_msg="m %s step %d" % (kk, it + 1))
+            np.testing.assert_allclose(got["v"].cpu().numpy(), vs, atol=TOL, err_msg="v %s step %d" % (kk, it + 1))
 
 
 @pytest.mark.parametrize("mode", ["sparse", "dense", "local"])

@@ -141,6 +141,58 @@ def test_oracle_gradient_matches_finite_differences(model, score, loss):
             assert abs(fd - g.reshape(-1)[j]) <= 1e-6 * max(1.0, abs(fd)), (name, j, fd, g.reshape(-1)[j])
 
 
+@pytest.mark.parametrize("model", ["TransE", "RESCAL", "TransH"])
+def test_oracle_adam_three_steps_match_eager_plugin_path(model, monkeypatch):
+    """keras Adam at t = 1, 2, 3 (BaseModel.py:243-246,328): the oracle's slot
+    state carried across calls == the package's eager plugin path (a separate
+    restatement: per-lookup IndexedSlices, unique-row scatter of the slots)
+    on the same injected negatives; sparse (TransE) and dense (RESCAL, TransH
+    regularisers) variables; and t = 2 differs from a restart at t = 1."""
+    monkeypatch.setenv("KGE_BACKEND", "eager")
+    from KGE import engine, loss, optimizers, score
+    from KGE.models.semantic_based.RESCAL import RESCAL
+    from KGE.models.translating_based.TransE import TransE
+    from KGE.models.translating_based.TransH import TransH
+    from KGE.ns_strategy import UniformStrategy
+    from tests.golden.make_golden import case_weights
+    rng = np.random.default_rng(4)
+    E, R, d, B, K = 9, 3, 5, 4, 4
+    W = case_weights(model, E, R, d, rng)
+    ns = UniformStrategy(np.arange(E), seed=1)
+    lf = loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0)
+    if model == "TransE":
+        m = TransE({"embedding_size": d}, K, "h+t", score_fn=score.LpDistance(2), loss_fn=lf, ns_strategy=ns)
+        sc = ("lp", 2.0)
+    elif model == "TransH":
+        m = TransH({"embedding_size": d}, K, "h+t", score_fn=score.LpDistancePow(2), loss_fn=lf, ns_strategy=ns,
+                   constraint_weight=0.3)
+        sc = ("lppow", 2.0)
+    else:
+        m = RESCAL({"embedding_size": d}, K, "h+t", loss_fn=lf, ns_strategy=ns, constraint_weight=0.5)
+        sc = ("dot", 0.0)
+    m.metadata = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
+    m.model_weights = {k: torch.tensor(v, dtype=torch.float64) for k, v in W.items()}
+    opt = optimizers.Adam(0.01)
+    ref_w, state = W, None
+    for it in range(3):
+        pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1)
+        neg = rng.integers(0, E, B * K)
+        negt = torch.tensor(orc.corrupt(pos, neg, K, "h+t"))
+        engine.eager_step(m, torch.tensor(pos), True, opt, neg=negt)
+        ref = orc.train_step(model, ref_w, pos, neg, score=sc, loss=("sans", 3.0, 1.0), lr=0.01, optimizer="adam",
+                             adam_state=state, constraint_weight=getattr(m, "constraint_weight", 1.0))
+        if it == 1:   # the slots matter: a fresh optimizer at t = 1 gives a different step
+            fresh = orc.train_step(model, ref_w, pos, neg, score=sc, loss=("sans", 3.0, 1.0), lr=0.01,
+                                   optimizer="adam", constraint_weight=getattr(m, "constraint_weight", 1.0))
+            assert max(np.abs(fresh["weights"][k] - ref["weights"][k]).max() for k in W) > 1e-4
+        ref_w, state = ref["weights"], ref["adam"]
+        for k, v in ref_w.items():
+            np.testing.assert_allclose(m.model_weights[k].numpy(), v, rtol=1e-9, atol=1e-12, err_msg="%s %d" % (k, it))
+        for k, (ms, vs) in state["slots"].items():
+            np.testing.assert_allclose(opt.slots[k]["m"].numpy(), ms, rtol=1e-9, atol=1e-15)
+            np.testing.assert_allclose(opt.slots[k]["v"].numpy(), vs, rtol=1e-9, atol=1e-18)
+
+
 # ---------------------------------------------------------------- reference property tests
 def test_scores_properties():
     """reference tests/test_score.py:7-50: Lp scores <= 0, finite, one per row (also complex)."""
