@@ -17,6 +17,13 @@ Other legs (``--workload``; one JSON line each, same schema):
   c5         TransE d=512 on a synthetic 50M-entity / 1000-relation graph with Zipf(1.1) heads /
              tails and Zipf(1.2) relations, entity table row-sharded (e mod N)
              through KGE/sharded.py's sparse all-to-all exchange at every N (N = 1 included)
+  c1-train / c2-train
+             the C1 / C2 configuration through the reference's entry point KGEModel.train
+             (example_fit_from_numpy.py:22-30 call pattern, BaseModel.py:58-190): wall time of
+             whole epochs per batch (device input stream, step, per-epoch loss read, histogram,
+             checkpoint), next to the same model's bare FusedStep time
+  eval       KGEModel.evaluate (BaseModel.py:578-654) of the C2 model on FB15k-237 valid_indexed
+             (17,526 triples), filtered by train + valid, corrupt_side 'h' and 't' (kge_rank)
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
 one process per GPU, each with its own 1024-positive batch (weak scaling, the
@@ -59,7 +66,8 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 F32_MFMA_PEAK_TF = 157.3   # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
 
-WORKLOADS = ("c2", "c1", "c3", "c4-rescal", "c4-transr", "c2-50m", "c5")
+WORKLOADS = ("c2", "c1", "c3", "c4-rescal", "c4-transr", "c2-50m", "c5", "c1-train", "c2-train", "eval")
+F32_VALU_PEAK_TF = 157.3   # MI355X fp32 vector peak (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -75,6 +83,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hbm-point", action="store_true",
                     help="c2 at one GPU: skip the live C2-50M (HBM-honest) KS measurement in roofline.hbm_point")
+    ap.add_argument("--epochs", type=int, default=2, help="c1-train / c2-train: timed epochs (after one warm-up)")
     ap.add_argument("--force-exchange", action="store_true",
                     help="one GPU: run the multi-GPU step (c5: all-to-all exchange + row cache instead of the "
                          "one-rank shortcut; other workloads: the sharded step with its exchange) as a rehearsal")
@@ -343,6 +352,157 @@ def pmc_traffic(workload):
         return None
 
 
+# ---------------------------------------------------------------- entry-point legs
+def _emit(out):
+    _RESULT_OUT.write(json.dumps(out) + "\n")
+    _RESULT_OUT.flush()
+
+
+def train_leg(args, dev):
+    """c1-train / c2-train: KGEModel.train as the reference's example calls it
+    (example_fit_from_numpy.py:22-30: index -> Model(...).train(train_X, ...,
+    epochs, batch_size, optimizer, seed)), on FB15k-237 train_indexed with
+    metadata ind2ent = range(E). One warm-up train() call of
+    one epoch, then one timed call of --epochs epochs; ms_per_step = its wall
+    time / batches. The same model's bare FusedStep is timed after it."""
+    import tempfile
+    from KGE import engine, optimizers
+    from KGE.models.translating_based.TransE import TransE
+    from KGE.ns_strategy import UniformStrategy
+    base = args.workload.split("-")[0]
+    w = spec(base, args)
+    triples, E, R = load_graph()
+    B, K, d = w["B"], w["K"], w["d"]
+    meta = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
+    model = TransE({"embedding_size": d}, K, w["side"], score_fn=w["score"], loss_fn=w["loss"],
+                   ns_strategy=UniformStrategy, constraint=w["constraint"])
+    per_epoch = {"histogram": 0.0, "checkpoint": 0.0}
+
+    def timed(name, fn):
+        def run(*a, **k):
+            t = time.perf_counter()
+            r = fn(*a, **k)
+            per_epoch[name] += time.perf_counter() - t
+            return r
+        return run
+    model._log_embeddings_histogram = timed("histogram", model._log_embeddings_histogram)
+    model._save_checkpoint = timed("checkpoint", model._save_checkpoint)
+    nb = int(math.ceil(len(triples) / B))
+    with tempfile.TemporaryDirectory() as logdir:
+        model.train(train_X=triples, val_X=None, metadata=meta, epochs=1, batch_size=B,
+                    optimizer=optimizers.SGD(0.01), seed=12345, log_path=logdir)
+        torch.cuda.synchronize()
+        for k in per_epoch:
+            per_epoch[k] = 0.0
+        t0 = time.perf_counter()
+        model.train(train_X=triples, val_X=None, metadata=meta, epochs=args.epochs, batch_size=B,
+                    optimizer=optimizers.SGD(0.01), seed=12345, log_path=logdir)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+    steps = args.epochs * nb
+    ms = wall * 1e3 / steps
+    # the bare fused step of the same model on the same batches (the c1 / c2 legs' number)
+    step = engine.FusedStep(model)
+    opt = optimizers.SGD(0.01)
+    g = torch.Generator().manual_seed(7)
+    idx = torch.randint(0, len(triples), (220, B), generator=g)
+    batches = torch.from_numpy(triples)[idx].to(dev)
+    for s in range(20):
+        step(batches[s], True, opt)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(20, 220):
+        step(batches[s], True, opt)
+    torch.cuda.synchronize()
+    fused_ms = (time.perf_counter() - t0) * 1e3 / 200
+    hist_ms = per_epoch["histogram"] * 1e3 / args.epochs
+    ckpt_ms = per_epoch["checkpoint"] * 1e3 / args.epochs
+    loop_ms = (wall * 1e3 - (hist_ms + ckpt_ms) * args.epochs) / steps
+    _emit({"metric": "positive-triples/sec through KGEModel.train (wall, whole epochs) at d=%d, FB15k-237" % d,
+           "value": round(B / (ms * 1e-3), 1), "unit": "positive-triples/s", "n_gpus": 1, "steps": steps,
+           "warmup": nb, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f32", "data": "FB15k-237 train_indexed (real graph), reference init",
+           "config": {"workload": "%s through KGEModel.train: %s" % (base.upper(), w["desc"] % dict(B=B, K=K, d=d)),
+                      "epochs": args.epochs, "batches_per_epoch": nb, "global_batch": B, "negatives": K, "dim": d,
+                      "parallelism": "dp1"},
+           "train_entry": {"ms_per_batch_wall": round(ms, 5), "ms_per_batch_loop": round(loop_ms, 5),
+                           "fused_step_ms": round(fused_ms, 5),
+                           "host_overhead_ms_per_batch": round(loop_ms - fused_ms, 5),
+                           "per_epoch_ms": {"histogram": round(hist_ms, 3), "checkpoint": round(ckpt_ms, 3)}},
+           "roofline": None, "cpu_baseline": None})
+
+
+def eval_leg(args, dev):
+    """eval: KGEModel.evaluate (BaseModel.py:578-618, get_rank :620-654) of the
+    C2 TransE model (reference init, d=200) on FB15k-237 valid_indexed, the
+    filter = train + valid positives; both corrupt sides, whole set per call
+    (kge_rank). Roofline: rank_count_kernel is VALU-bound (3 flops per
+    candidate element: subtract, fused square-accumulate) -- n x E x d x 3
+    flops per side against the fp32 vector peak."""
+    from KGE import ranking
+    from KGE.models.translating_based.TransE import TransE
+    from KGE.ns_strategy import UniformStrategy
+    w = spec("c2", args)
+    triples, E, R = load_graph()
+    V = np.load(os.path.join(ROOT, "data", "fb15k237_valid.npz"))["triples"].astype(np.int64)
+    d = w["d"]
+    model = TransE({"embedding_size": d}, w["K"], w["side"], score_fn=w["score"], loss_fn=w["loss"],
+                   ns_strategy=UniformStrategy(np.arange(E), seed=1), constraint=w["constraint"])
+    model.metadata = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
+    model._model_weights_initial = None
+    model._init_embeddings(seed=12345)
+    model._to_device()
+    assert ranking.supported(model)
+    P = np.concatenate([triples.astype(np.int64), V])
+    model.evaluate(V[:512], "t", P)       # warm-up (library load, kernels)
+    torch.cuda.synchronize()
+    sides = {}
+    for side in ("h", "t"):
+        t0 = time.perf_counter()
+        res = model.evaluate(V, side, P)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        ranking.batched_ranks(model, V, side, P)
+        ev[1].record()
+        torch.cuda.synchronize()
+        sides[side] = {"evaluate_s": round(wall, 5), "device_ms": round(ev[0].elapsed_time(ev[1]), 4),
+                       "mrr": round(res["mean_reciprocal_rank"], 6), "hit@10": round(res["hit@10"], 6)}
+    n = len(V)
+    tot = sides["h"]["evaluate_s"] + sides["t"]["evaluate_s"]
+    dev_ms = sides["h"]["device_ms"] + sides["t"]["device_ms"]
+    flops = 2 * n * E * d * 3.0
+    cpu = None
+    if not args.no_cpu_baseline:
+        # the reference's per-triple get_rank loop restated on the host (torch CPU, same model)
+        cm = TransE({"embedding_size": d}, w["K"], w["side"], score_fn=w["score"], loss_fn=w["loss"],
+                    ns_strategy=UniformStrategy(np.arange(E), seed=1), constraint=w["constraint"])
+        cm.metadata = model.metadata
+        cm.model_weights = {k: v.detach().cpu() for k, v in model.model_weights.items()}
+        threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1, os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        k, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < min(args.cpu_seconds, 10.0):
+            cm.get_rank(V[k % n], P, "t")
+            k += 1
+        cpu = {"value": k / (time.perf_counter() - t0), "unit": "ranked-triples/s", "cores": threads,
+               "kind": "port", "sample": "%d triples of FB15k-237 valid through the per-triple get_rank loop "
+                                         "(BaseModel.py:620-654 restated, torch CPU), filtered, side 't'" % k}
+    _emit({"metric": "filtered ranked triples/sec (KGEModel.evaluate, both sides) at d=%d, FB15k-237 valid" % d,
+           "value": round(2 * n / tot, 1), "unit": "ranked-triples/s", "n_gpus": 1, "steps": 2, "warmup": 1,
+           "ms_per_step": round(tot * 1e3 / 2, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f32",
+           "data": "FB15k-237 valid_indexed (%d triples), filter train + valid; reference-init weights" % n,
+           "config": {"workload": "evaluate(): TransE d=%d LpDistance(2), E=%d candidates per query, both sides"
+                                  % (d, E), "sides": sides, "parallelism": "dp1"},
+           "roofline": {"bound": "valu", "kernel": "rank_count_kernel (+ pos / filter passes)",
+                        "achieved": round(flops / (dev_ms * 1e-3) / 1e12, 2), "peak": F32_VALU_PEAK_TF,
+                        "unit": "TFLOP/s", "frac": round(flops / (dev_ms * 1e-3) / 1e12 / F32_VALU_PEAK_TF, 4),
+                        "flops": flops, "traffic": None},
+           "cpu_baseline": cpu})
+
+
 # ---------------------------------------------------------------- main
 def main():
     args = parse()
@@ -358,6 +518,10 @@ def main():
 
     from KGE import _hip, engine
     _hip.load()   # the shipped gfx950 library; raises if missing
+    if args.workload in ("c1-train", "c2-train"):
+        return train_leg(args, dev)
+    if args.workload == "eval":
+        return eval_leg(args, dev)
 
     w = spec(args.workload, args)
     triples, E, R = load_graph()

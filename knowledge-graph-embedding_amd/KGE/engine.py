@@ -157,6 +157,7 @@ class FusedStep:
         self.workspace = torch.empty(0, dtype=torch.uint8, device=dev)
         self.grads = None
         self.batch_scale = 1.0
+        self.cw_scale = 1.0           # multi-GPU: share of a full-table regulariser this rank adds
         self.flags = 0
         self.plane_fn = None          # optional: planes -> first plane (multi-GPU offsets)
         self.shard = None             # optional (G, shard_rows, global E): the tables are gathered shards
@@ -229,7 +230,7 @@ class FusedStep:
         d.temperature = temp
         d.batch_scale = self.batch_scale
         d.constraint = int(bool(getattr(m, "constraint", False)))
-        d.constraint_weight = float(getattr(m, "constraint_weight", 0.0))
+        d.constraint_weight = float(getattr(m, "constraint_weight", 0.0)) * self.cw_scale
         d.rotate_limit = float(t.get("limit", 0.0))
         d.optimizer = self._opt_code(is_train, optimizer)
         if d.optimizer == _hip.OPT_SGD:
@@ -269,7 +270,8 @@ class FusedStep:
                tuple((t[r].data_ptr(), tuple(t[r].shape), t[r].stride(0)) if t.get(r) is not None else None
                      for r in ("ent", "rel", "ent_aux", "rel_aux")),
                tuple((g.data_ptr(), tuple(g.shape)) for g in self.grads) if self.grads is not None else None,
-               id(m.ns_strategy), m.negative_ratio, m.corrupt_side, self.batch_scale, self.flags)
+               id(m.ns_strategy), m.negative_ratio, m.corrupt_side, self.batch_scale, self.cw_scale, self.flags,
+               float(getattr(m, "constraint_weight", 0.0)))
         cached = getattr(self, "_cache", None)
         if cached is not None and cached[0] == key:
             d = cached[1]

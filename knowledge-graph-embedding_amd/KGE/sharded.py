@@ -110,13 +110,19 @@ class ShardedStep:
         dev = ent.device
         self.device = dev
         self.mid = model._fused_model_id
-        if self.mid == _hip.MODEL_RESCAL or (self.mid == _hip.MODEL_TRANSH and getattr(model, "constraint", False)):
-            raise NotImplementedError("sharded step: full-table regulariser gradients (RESCAL, TransH with "
-                                      "constraint) are not sharded in this build")
+        # full-table regularisers (RESCAL.py:190-198, TransH.py:202-211 with
+        # constraint) make TF's gradients dense: every rank adds 1/G of the
+        # term (loss and gradient) to its replica's gradient, the all-reduce
+        # sums them, and the clip norm is taken of the reduced dense tensor
+        self.full_reg = self.mid == _hip.MODEL_RESCAL or (self.mid == _hip.MODEL_TRANSH and
+                                                           bool(getattr(model, "constraint", False)))
         if mode == "auto":
-            mode = "dense" if E * C * 4 <= DENSE_TABLE_BYTES else "sparse"
+            mode = "dense" if E * C * 4 <= DENSE_TABLE_BYTES or self.full_reg else "sparse"
         if mode not in ("dense", "sparse"):
             raise ValueError("mode must be 'auto', 'dense' or 'sparse'")
+        if mode == "sparse" and self.full_reg:
+            raise NotImplementedError("sharded step: a full-table regulariser (RESCAL, TransH with constraint) "
+                                      "has a dense gradient of every row -- use the dense exchange")
         self.mode = mode
         if mode == "sparse":
             # owned rows [ent | ent_aux], padded to Es rows
@@ -155,6 +161,8 @@ class ShardedStep:
             f.loss_out = self.loss
             f.status = self.status
             f.batch_scale = float(G)
+            if self.full_reg:
+                f.cw_scale = 1.0 / G
             f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT
             if mode == "sparse":   # every cache row [0, U) is a batch id: no gradient zero-fill
                 f.flags |= _hip.FLAG_GRAD_ROWS_TOUCHED
@@ -208,6 +216,9 @@ class ShardedStep:
             if self.clip:
                 rows.copy_(clip_constraint(rows, p=2, value=1, axis=-1))
                 rel.copy_(clip_constraint(rel, p=2, value=1, axis=-1))
+            if self.hyper:
+                w = self.tables["rel_aux"]
+                w.copy_(normalized_embeddings(w, p=2, value=1, axis=1))
 
     def _draw(self, batch):
         """Negatives in the step's slot layout (h+t: alternating h / t draws,
@@ -300,14 +311,19 @@ class ShardedStep:
         # host-only (KGE_BACKEND=eager) restatement of the same phase, for the gloo tests
         m = self.model
         saved = dict(m.model_weights)
+        cw = getattr(m, "constraint_weight", None)
         try:
             m.model_weights[self.names["ent"]] = lt["ent"]
             if self.ca:
                 m.model_weights[self.names["ent_aux"]] = lt["ent_aux"]
+            if self.full_reg:
+                m.constraint_weight = cw / self.G
             loss, grads = engine.eager_grads(m, batch, is_train, neg=self._neg_triples(batch, neg),
                                              batch_scale=float(self.G))
         finally:
             m.model_weights.update(saved)
+            if self.full_reg:
+                m.constraint_weight = cw
         self.red.zero_()
         for b in gbufs:
             b.zero_()
@@ -431,6 +447,13 @@ class ShardedStep:
             # one all-reduce and the same apply on every rank
             self._local_grads(batch, neg_ids, is_train, optimizer, dict(self.tables), self.gent, prof_events)
             self.ex.all_reduce(self.red)
+            if is_train and self.full_reg:
+                # dense variables: clip_by_norm of the reduced tensor (norms
+                # do not add across ranks); identical on every rank
+                dense = [(0, self.gent[0])] + [(1 if r == "rel" else 2, self.grel[r]) for r in self.rel_roles]
+                for slot, gbuf in dense:
+                    g1 = gbuf.reshape(-1)
+                    self.norm2[slot:slot + 1].copy_(torch.dot(g1, g1).reshape(1))
             if is_train:
                 for k, gk in enumerate(self.gent):
                     self._apply_dense(self._ent_rows(k), gk, self._slot(k), optimizer,

@@ -211,6 +211,10 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   // workgroup
   int wpp = 1;
   while (wpp < kStepWaves && ((int64_t)wpp * KGE_SLOTS_PER_WAVE < Keff || kStepWaves % wpp != 0)) ++wpp;
+  // small grids (C4: 512 positives x 64 negatives gave 64 workgroups for 256
+  // CUs): spread each positive's slots over more waves while the grid has
+  // fewer than two workgroups per CU and every wave keeps >= 8 slots
+  while (wpp < kStepWaves && ceil_div(B, kStepWaves / wpp) < 512 && Keff >= 16 * wpp) wpp *= 2;
   const int nP = kStepWaves / wpp;
   // 'h+t': even slot ranges, so every stream batch starts on an h-corrupt slot
   int SW = std::max<int>(1, (int)ceil_div(Keff, wpp));

@@ -235,6 +235,7 @@ template <int VEC, int NC, int SK>
 struct TransE {
   static constexpr bool CPLX = false;
   static constexpr bool WIDE = false;   // score kernel fits 128 VGPRs at one chunk (4 waves / SIMD)
+  static constexpr bool SELF_CTX = false;   // context rows computed by the score kernel itself (RESCAL)
   static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
@@ -385,6 +386,7 @@ template <int VEC, int NC, int SK_UNUSED>
 struct DistMult {
   static constexpr bool CPLX = false;
   static constexpr bool WIDE = true;    // five context rows: 256-VGPR budget (2 waves / SIMD)
+  static constexpr bool SELF_CTX = false;
   static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
@@ -467,6 +469,7 @@ template <int VEC, int NC, int SK>
 struct RotatE {
   static constexpr bool CPLX = true;
   static constexpr bool WIDE = true;
+  static constexpr bool SELF_CTX = false;
   static constexpr bool MAT = false;
   static constexpr int NSNAP = 3;
   static constexpr int HV = VEC / 2;
@@ -583,23 +586,26 @@ struct RotatE {
 
 // ======================================================================
 // RESCAL: h^T R_r t     (RESCAL.py:140-174); score_fn not used
-// The relation matrix never enters the score kernel: a separate MFMA pass
-// (kge_rel.hip) writes each positive's context rows u = R^T h (snap row 0)
-// and v = R t (snap row 1) first, so every triple of the positive is a dot
-// product of two d-vectors:
+// A positive's score waves first compute its context rows u = R^T h and
+// v = R t together (rel_gemv_pair, kge_step_impl.h: R_r streamed once per
+// positive from L2, rows split over the waves), so every triple of the
+// positive is a dot product of two d-vectors:
 //   positive      u . t
 //   t-corrupted   u . e          (gradient wrt e: alpha u)
 //   h-corrupted   e . v          (gradient wrt e: alpha v)
 // The positive's own rows need R again: g_h = R (c_p t + sum_tc alpha e),
-// g_t = R^T (c_p h + sum_hc alpha e). The score kernel therefore leaves the
-// UN-projected sums in the positive-gradient rows -- row 0: A = c_p t +
-// sum_tc alpha e, row 1: b = sum_hc alpha e, row 2: B = c_p h + b -- and the
-// MFMA pass after it projects them and forms dR_r = sum_i h_i (x) A_i + b_i (x) t_i.
+// g_t = R^T (c_p h + sum_hc alpha e) -- the same waves after the merge, from
+// the UN-projected sums in the positive-gradient rows (row 0: A = c_p t +
+// sum_tc alpha e, row 1: b = sum_hc alpha e, row 2: B = c_p h + b). The MFMA
+// pass after the score kernel forms dR_r = sum_i h_i (x) A_i + b_i (x) t_i.
 // ======================================================================
 template <int VEC, int NC, int SK_UNUSED>
 struct Rescal {
   static constexpr bool CPLX = false;
   static constexpr bool WIDE = false;
+  // u = R^T h, v = R t computed by the positive's own score waves (and the
+  // post products g_h = R A, g_t = R^T B after the merge): no separate passes
+  static constexpr bool SELF_CTX = true;
   static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
@@ -668,6 +674,7 @@ template <int VEC, int NC, int SK_UNUSED>
 struct Materialised {
   static constexpr bool CPLX = false;
   static constexpr bool WIDE = false;
+  static constexpr bool SELF_CTX = false;
   static constexpr bool MAT = true;
   static constexpr int NSNAP = 0;
   static constexpr bool NRM_FROM_R = false;

@@ -2,20 +2,19 @@
 //
 // RESCAL scores h^T R_r t with a dense d x d matrix per relation
 // (RESCAL.py:140-174). Every triple of a positive shares (h, R_r) or
-// (R_r, t), so the matrix work is per POSITIVE, not per negative:
+// (R_r, t), so the matrix work is per POSITIVE, not per negative: the score
+// kernel's waves form a positive's context rows u = R^T h, v = R t and, after
+// its merge, the positive's own row gradients g_h = R A, g_t = R^T B
+// (rel_gemv_pair, kge_step_impl.h). This file holds the per-relation passes:
 //
 //   KR  rank      positives stably sorted by relation (one pass, no atomics),
 //                 so every relation's positives are contiguous.
-//   KC  context   u_i = R^T h_i and v_i = R t_i for 16 positives of one
-//                 relation at a time: two [16 x d] x [d x d] products on
-//                 v_mfma_f32_16x16x4_f32. The score kernel then streams the
-//                 negatives as dot products (u . e, e . v).
-//   KP  post      the positives' own row gradients g_h = R A_i, g_t = R^T B_i
-//                 (same tile shape), and per relation dR_r = sum_i h_i (x) A_i
-//                 + b_i (x) t_i as [d x 2n] x [2n x d] MFMA tiles, plus the
-//                 dense regulariser term (2 lambda / R) R_r of every relation
-//                 (RESCAL.py:190-198) and the dense gradient's norm^2.
-//   KL  reg loss  lambda (mean_e ||e||^2 + mean_r ||R_r||_F^2) added to the loss.
+//   KP  dR        per relation dR_r = sum_i h_i (x) A_i + b_i (x) t_i as
+//                 [d x 2n] x [2n x d] MFMA tiles, plus the dense regulariser
+//                 term (2 lambda / R) R_r of every relation (RESCAL.py:190-198)
+//                 and the dense gradient's norm^2.
+//   KL  reg loss  lambda (mean_e ||e||^2 + mean_r ||R_r||_F^2) added to the loss
+//                 (validation steps; train steps fold it into KP and the update).
 //
 // MFMA operand maps (v_mfma_f32_16x16x4_f32, one f32 per lane): lane l holds
 // A[l & 15][k = l >> 4] and B[k = l >> 4][l & 15]; the 4 accumulators hold
@@ -116,102 +115,6 @@ __global__ __launch_bounds__(256) void rel_rank_wave_kernel(RelArgs P) {
     if (dor) {
       P.rel_beg[t] = rlt;
       P.rel_cnt[t] = rcnt;
-    }
-  }
-}
-
-// ------------------------------------------------------------ KC / KP pair products
-// Workgroup (p, g): p = a leading sorted position of a 16-positive tile of
-// one relation (other positions exit at once), g = a group of 4 of the
-// tile's 2 x ceil(d/16) output column tiles (one per wave). X1, X2 = the 16
-// staged input rows; each wave holds its column tile's whole B operand in
-// registers (inner dimension <= 256) before its MFMA chain.
-//   MODE 0 (context): X1 = h rows, X2 = t rows; out0 = X1 R (u), out1 = X2 R^T (v)
-//   MODE 1 (post):    X1 = B rows, X2 = A rows; out0 = X1 R (g_t), out1 = X2 R^T (g_h)
-template <int MODE>
-__global__ __launch_bounds__(256) void rel_pair_kernel(RelArgs P) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  // rows staged at DP = d rounded to 16 floats (zero padded): the MFMA inner
-  // dimension is split into 4 contiguous blocks of DP / 4 (a multiple of 4),
-  // lane group kq = lane >> 4 owning block kq, so a lane's B fragment of the
-  // transposed product (R^T) is a contiguous run of R's row -> float4 loads
-  const int d = P.d, DP = (d + 15) & ~15, nct = (d + 15) / 16;
-  const int njg = (2 * nct + 3) / 4;
-  const int64_t p = blockIdx.x / njg;
-  const int g = (int)(blockIdx.x % njg);
-  const int64_t r = P.srel[p];
-  const int64_t g0 = P.rel_beg[r];
-  if ((p - g0) % 16 != 0) return;
-  const int n = (int)min<int64_t>(16, g0 + P.rel_cnt[r] - p);
-  float* X1 = sm;
-  float* X2 = sm + 16 * DP;
-  __shared__ int64_t s_i[16];
-  __shared__ const float* s_x1[16];
-  __shared__ const float* s_x2[16];
-  if (threadIdx.x < 16) {   // each staged row's source, resolved once
-    const int q = threadIdx.x;
-    const int64_t i = q < n ? P.sorted[p + q] : 0;
-    s_i[q] = i;
-    if (MODE == 0) {
-      s_x1[q] = P.ent.row(pos_id(P, i, 0));
-      s_x2[q] = P.ent.row(pos_id(P, i, 2));
-    } else {
-      const float* gr = P.gpos + i * 3 * (int64_t)P.gcols;
-      s_x1[q] = gr + 2 * P.gcols;   // B_i
-      s_x2[q] = gr;                 // A_i
-    }
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < 16 * DP; e += blockDim.x) {
-    const int q = e / DP, k = e - q * DP;
-    const bool in = q < n && k < d;
-    X1[e] = in ? s_x1[q][k] : 0.f;
-    X2[e] = in ? s_x2[q][k] : 0.f;
-  }
-  const int lane = lane_id(), wv = wave_id();
-  const int job = g * 4 + wv;
-  const bool has_job = job < 2 * nct;
-  const int prod = job & 1, jt = job >> 1;
-  const int col = jt * 16 + (lane & 15), kq = lane >> 4;
-  const int nks = DP / 4;          // k-steps; step ks of lane group kq is k = kq * nks + ks
-  const int kb = kq * nks;
-  const float* Rm = P.rel.row(r);
-  const bool v4 = d % 4 == 0 && P.rel.ld % 4 == 0 && ((uintptr_t)P.rel.p % 16) == 0;
-  float bf[64];   // d <= 256 (plan check)
-  if (prod == 1 && v4) {
-    // R^T: B[k][col] = R[col][k], a contiguous run of row col
-#pragma unroll
-    for (int q4 = 0; q4 < 16; ++q4) {
-      const int k = kb + 4 * q4;   // d % 4 == 0: the 4 elements are all < d or all >= d
-      const float4 x = (has_job && 4 * q4 < nks && k < d && col < d)
-                           ? *reinterpret_cast<const float4*>(Rm + (int64_t)col * d + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-      bf[4 * q4] = x.x; bf[4 * q4 + 1] = x.y; bf[4 * q4 + 2] = x.z; bf[4 * q4 + 3] = x.w;
-    }
-  } else {
-#pragma unroll
-    for (int ks = 0; ks < 64; ++ks) {
-      const int k = kb + ks;
-      bf[ks] = (has_job && ks < nks && k < d && col < d)
-                   ? (prod == 0 ? Rm[(int64_t)k * d + col] : Rm[(int64_t)col * d + k]) : 0.f;
-    }
-  }
-  __syncthreads();
-  if (!has_job) return;
-  const float* xa = (prod ? X2 : X1) + (lane & 15) * DP + kb;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < 64; ++ks)
-    if (ks < nks) acc = mfma16(xa[ks], bf[ks], acc);
-  if (col < d) {
-#pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      const int row = kq * 4 + gg;
-      if (row >= n) continue;
-      const int64_t i = s_i[row];
-      float* out;
-      if (MODE == 0) out = P.snap + i * 2 * (int64_t)d + (prod ? d : 0);
-      else out = P.gproj + i * 2 * (int64_t)d + (prod ? 0 : d);
-      out[col] = acc[gg];
     }
   }
 }
@@ -462,17 +365,8 @@ void launch_rel_rank(const RelArgs& P, hipStream_t st) {
   else
     hipLaunchKernelGGL(rel_rank_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P);
 }
-static unsigned pair_grid(const RelArgs& P) {
-  const int nct = (P.d + 15) / 16;
-  return (unsigned)(P.B * ((2 * nct + 3) / 4));
-}
-void launch_rel_ctx(const RelArgs& P, hipStream_t st) {
-  const size_t lds = 2 * 16 * (size_t)((P.d + 15) & ~15) * sizeof(float);
-  hipLaunchKernelGGL(rel_pair_kernel<0>, dim3(pair_grid(P)), dim3(256), lds, st, P);
-}
 void launch_rel_post(const RelArgs& P, hipStream_t st) {
-  const size_t lds = 2 * 16 * (size_t)((P.d + 15) & ~15) * sizeof(float);
-  hipLaunchKernelGGL(rel_pair_kernel<1>, dim3(pair_grid(P)), dim3(256), lds, st, P);
+  // (g_h, g_t: the score kernel's waves, Rescal::SELF_CTX)
   const int nct = (P.d + 15) / 16;
   const size_t lds2 = (32 * 16 + 16 * (size_t)nct * 16) * sizeof(float);
   hipLaunchKernelGGL(rel_dr_kernel, dim3((unsigned)(P.rel.rows * nct)), dim3(256), lds2, st, P);

@@ -54,11 +54,11 @@ struct StepCtl {
 // entry (a scalar load: a launch of 10^5 waves must not queue 10^5 requests on
 // the one L2 channel that holds it -- an atomic load there cost C2-50M's
 // update kernel 120 us); it is written only with a vector store.
-__device__ __forceinline__ bool ws_refused(StepCtl* ctl, uint32_t sig, int32_t* status, float* loss_out) {
-  const uint32_t s = *reinterpret_cast<const uint32_t*>(&ctl->plan_sig);
+__device__ __noinline__ bool ws_refused_slow(StepCtl* ctl, uint32_t s, uint32_t sig, int32_t* status,
+                                             float* loss_out) {
   const bool lead = blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
-  if (s == 0u || s == sig) {
-    if (s == 0u && lead) __hip_atomic_store(&ctl->plan_sig, sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (s == 0u) {
+    if (lead) __hip_atomic_store(&ctl->plan_sig, sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return false;
   }
   if (lead) {
@@ -66,6 +66,13 @@ __device__ __forceinline__ bool ws_refused(StepCtl* ctl, uint32_t sig, int32_t* 
     if (loss_out) loss_out[0] = __builtin_nanf("");
   }
   return true;
+}
+__device__ __forceinline__ bool ws_refused(StepCtl* ctl, uint32_t sig, int32_t* status, float* loss_out) {
+  const uint32_t s = *reinterpret_cast<const uint32_t*>(&ctl->plan_sig);
+  // the common case (the workspace is this plan's) is one scalar compare; the
+  // claim / refusal path is out of line so it costs the kernel no registers
+  if (__builtin_expect(s == sig, 1)) return false;
+  return ws_refused_slow(ctl, s, sig, status, loss_out);
 }
 
 // Optimizer apply over a whole table (kge_apply, and the dense-gradient
@@ -219,8 +226,7 @@ struct RelArgs {
   float* loss_out;
 };
 void launch_rel_rank(const RelArgs& R, hipStream_t st);
-void launch_rel_ctx(const RelArgs& R, hipStream_t st);      // u, v
-void launch_rel_post(const RelArgs& R, hipStream_t st);     // g_h, g_t, dR (+ dense term, norm^2)
+void launch_rel_post(const RelArgs& R, hipStream_t st);     // dR (+ dense term, norm^2)
 // lambda * (mean_e ||e||^2 + mean_r ||R_r||_F^2) added to the step loss (RESCAL.py:190-198)
 void launch_reg_loss(const TabView& ent, const TabView& rel, float lam, float* part, StepCtl* ctl,
                      float* loss_out, float* loss_accum, uint32_t sig, int32_t* status, hipStream_t st);

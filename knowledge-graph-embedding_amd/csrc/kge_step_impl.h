@@ -39,6 +39,9 @@
 #ifndef KGE_STREAM_ROWS
 #define KGE_STREAM_ROWS 8   // sampled rows per stream batch at NC = 1 (tuning knob)
 #endif
+#ifndef KGE_COMPACT_LIST0
+#define KGE_COMPACT_LIST0 1 // compact launches: list position 0 lives only in the leader table (A-B knob)
+#endif
 #ifndef KGE_GUARD_KU
 #define KGE_GUARD_KU 1      // update kernel: workspace plan guard at entry (tuning / A-B knob)
 #endif
@@ -149,6 +152,9 @@ __device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_
         ? A.npos3 + (code >> A.kshift) * (uint32_t)A.Keff + (code & ((1u << A.kshift) - 1u))
         : 3u * ((code - A.nkeyneg) >> 2) + ((code - A.nkeyneg) & 3u);
     A.leaders[kpos] = make_uint4((uint32_t)dest, r == 0u ? code : 0xFFFFFFFFu, h, 0u);
+    // position 0's code is the leader table's (a 50M-row table's destinations
+    // mostly hold one key: no scattered list store for them at all)
+    if (KGE_COMPACT_LIST0 && r == 0u) return;
   } else {
     r = atomicAdd(&A.cnt[dest], 1u);
   }
@@ -203,6 +209,51 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 template <int SIDE>
 __host__ __device__ constexpr int kind_at(int u) {
   return SIDE == KGE_SIDE_HT ? ((u & 1) ? KIND_TC : KIND_HC) : SIDE == KGE_SIDE_H ? KIND_HC : KIND_TC;
+}
+
+// element i of a row fragment, as a wave-uniform scalar (i wave-uniform)
+template <int VEC, int NC>
+__device__ __forceinline__ float frag_elem_bcast(const Frag<VEC, NC>& f, int i) {
+  const int c = i / (KGE_WAVE * VEC), rem = i - c * KGE_WAVE * VEC;
+  const int q = c * VEC + rem % VEC;
+  float v = 0.f;
+#pragma unroll
+  for (int k = 0; k < VEC * NC; ++k) v = k == q ? f.v[k] : v;
+  return bcast(v, rem / VEC);
+}
+
+// RESCAL context products of one positive (RESCAL.py:166-171), shared by its
+// waves: this wave takes rows [rb, re) of R (row i at Rm + i d) in batches
+// of 8 (every row's load issued before use) and accumulates
+//   u-like  up += x_i R_i            (u = R^T x: the wave's partial)
+//   v-like  vl[i] = R_i . y          (v = R y: one transposed 8-row reduction)
+// The callers sum the waves' partials of u in wave order (LDS).
+template <int VEC, int NC>
+__device__ void rel_gemv_pair(const float* __restrict__ Rm, int d, int rb, int re, const Frag<VEC, NC>& x,
+                              const Frag<VEC, NC>& y, Frag<VEC, NC>& up, float* vl) {
+  using F = Frag<VEC, NC>;
+  constexpr int NB = 8, SH = 3;
+  up.zero();
+  for (int i0 = rb; i0 < re; i0 += NB) {
+    F Rr[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) load_row(Rr[u], Rm + (int64_t)min(i0 + u, re - 1) * d, d);
+    float part[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const float xi = i0 + u < re ? frag_elem_bcast(x, i0 + u) : 0.f;
+      float p = 0.f;
+#pragma unroll
+      for (int q = 0; q < VEC * NC; ++q) {
+        up.v[q] += xi * Rr[u].v[q];
+        p += Rr[u].v[q] * y.v[q];
+      }
+      part[u] = p;
+    }
+    const float vr = multi_reduce<NB, false>(part);
+    const int u = lane_id() >> SH;
+    if ((lane_id() & ((1 << SH) - 1)) == 0 && i0 + u < re) vl[i0 + u] = vr;
+  }
 }
 
 // per-positive merge slots (LDS)
@@ -289,8 +340,51 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   F accH, accR, accT;
   accH.zero(); accR.zero(); accT.zero();
   float Rp = 0.f, tp = 1.f, sp = 0.f, lpp = 0.f;
-  if (active) {
+  if constexpr (M::SELF_CTX) {
+    // the positive's waves compute its context rows together (Rescal):
+    // u = R^T h (waves' partials summed in wave order), v = R t (each entry
+    // from the wave owning its row) -- through the wave's slices of `red`
+    const int d = A.ent.cols;
+    const int rpw = ((d + wpp - 1) / wpp + 7) & ~7;
+    const int rb = min(d, gw * rpw), re = min(d, rb + rpw);
+    float* myred = red + wv * 3 * FL;
+    for (int e = lane; e < FL; e += KGE_WAVE) myred[FL + e] = 0.f;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    F up;
+    up.zero();
+    if (active) {
+      load_row(ctx.H, A.ent.row(ph), d);
+      load_row(ctx.T, A.ent.row(pt), d);
+      rel_gemv_pair<VEC, NC>(A.rel.row(pr), d, rb, re, ctx.H, ctx.T, up, myred + FL);
+    }
+#pragma unroll
+    for (int q = 0; q < VEC * NC; ++q) myred[(q / VEC * KGE_WAVE + lane) * VEC + q % VEC] = up.v[q];
+    __syncthreads();
+    if (active) {
+      ctx.U.zero();
+      ctx.V.zero();
+      for (int g = 0; g < wpp; ++g) {
+        const float* gr = red + (grp * wpp + g) * 3 * FL;
+#pragma unroll
+        for (int q = 0; q < VEC * NC; ++q) {
+          const int e = (q / VEC * KGE_WAVE + lane) * VEC + q % VEC;
+          ctx.U.v[q] += gr[e];
+          ctx.V.v[q] += gr[FL + e];
+        }
+      }
+      if (gw == 0 && A.train) {   // the update kernel's context rows (snap)
+        float* sn = A.snap + i * (M::NSNAP * (int64_t)A.snap_cols);
+        store_row(ctx.U, sn, d);
+        store_row(ctx.V, sn + A.snap_cols, d);
+      }
+    }
+    __syncthreads();   // `red` is reused for the wave states below
+  } else if (active) {
     M::load_ctx(ctx, A.ent, A.rel, ph, pr, pt, mp);
+  }
+  if (active) {
     {   // the positive's score, in every wave (hinge / logistic weights need it)
       F a, b, E0;
       E0.zero();
@@ -572,6 +666,57 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
       for (int g = 0; g < wpp; ++g) s += mg[MG_F + g] * red[((p * wpp + g) * 3 + v) * FL + src];
       if (v == 1 && A.rel_reg != 0.f) s += (A.rel_reg * A.inv_b) * (2.f * A.rel.row(s_pos[p * 3 + 1])[k]);
       A.gpos[(i0 + p) * 3 * (int64_t)A.gcols + v * (int64_t)A.gcols + k] = s;
+      if constexpr (M::SELF_CTX) posg[(p * 3 + v) * FL + k] = s;   // (read just above by this thread only)
+    }
+  }
+  if constexpr (M::SELF_CTX) {
+    if (A.train) {
+      // the positive's own entity-row gradients g_h = R A, g_t = R^T B
+      // (A = row 0, B = row 2 of its gradient sums), the same split of R's
+      // rows over its waves; written where the update kernel reads them (gpe)
+      __syncthreads();
+      const int d = A.ent.cols;
+      const int rpw = ((d + wpp - 1) / wpp + 7) & ~7;
+      const int rb = min(d, gw * rpw), re = min(d, rb + rpw);
+      float* myred = red + wv * 3 * FL;
+      for (int e = lane; e < FL; e += KGE_WAVE) myred[FL + e] = 0.f;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      F up;
+      up.zero();
+      if (active) {
+        F Ar, Br;
+        const float* pa = posg + (grp * 3 + 0) * FL;
+        const float* pb = posg + (grp * 3 + 2) * FL;
+#pragma unroll
+        for (int q = 0; q < VEC * NC; ++q) {
+          const int e = (q / VEC * KGE_WAVE + lane) * VEC + q % VEC;
+          Ar.v[q] = e < d ? pa[e] : 0.f;
+          Br.v[q] = e < d ? pb[e] : 0.f;
+        }
+        rel_gemv_pair<VEC, NC>(A.rel.row(pr), d, rb, re, Br, Ar, up, myred + FL);
+      }
+#pragma unroll
+      for (int q = 0; q < VEC * NC; ++q) myred[(q / VEC * KGE_WAVE + lane) * VEC + q % VEC] = up.v[q];
+      __syncthreads();
+      if (active && gw == 0) {
+        F gh, gt;
+        gh.zero();
+        gt.zero();
+        for (int g = 0; g < wpp; ++g) {
+          const float* gr = red + (grp * wpp + g) * 3 * FL;
+#pragma unroll
+          for (int q = 0; q < VEC * NC; ++q) {
+            const int e = (q / VEC * KGE_WAVE + lane) * VEC + q % VEC;
+            gt.v[q] += gr[e];
+            gh.v[q] += gr[FL + e];
+          }
+        }
+        float* go = A.gpe + i * (int64_t)A.gpe_stride;
+        store_row(gh, go, d);
+        store_row(gt, go + A.gpe_toff, d);
+      }
     }
   }
 
@@ -706,9 +851,6 @@ void update_kernel(StepArgs A) {
   __shared__ uint32_t s_scr[kUpdWaves][CHMAX * KGE_WAVE];
   __shared__ uint32_t s_sort[kUpdWaves][kSortMax];    // longer lists: gathered + bitonic-sorted here
 
-#if KGE_GUARD_KU
-  if (ws_refused(A.ctl, A.sig, A.status, A.loss_out)) return;
-#endif
   KGE_PROF_INIT();
   const int lane = lane_id(), wv = wave_id();
   const int64_t E_ = A.ent.rows;
@@ -720,15 +862,20 @@ void update_kernel(StepArgs A) {
   int64_t d, li;   // destination row, its list index (the row, or its hash slot)
   bool active;
   uint32_t code1 = 0xFFFFFFFFu;   // compact: the destination's first filed code
+  // workspace guard (ws_refused): the step's first kernel claimed the
+  // workspace for this plan or refused it (and reported); here a refused
+  // workspace just leaves every wave idle -- one scalar compare, no branch
+  // of its own (an early return cost the compact instance registers)
+  const bool ws_ok = !KGE_GUARD_KU || *reinterpret_cast<const uint32_t*>(&A.ctl->plan_sig) == A.sig;
   if (A.compact) {   // one wave per key position: the destinations' first keys lead
     // (read unconditionally: the array is padded to the grid)
     const uint4 t = A.leaders[dd];
-    active = dd < (int64_t)A.nkeys && t.y != 0xFFFFFFFFu && !(A.rel_only && (int64_t)t.x < E_);
+    active = ws_ok && dd < (int64_t)A.nkeys && t.y != 0xFFFFFFFFu && !(A.rel_only && (int64_t)t.x < E_);
     d = active ? (int64_t)t.x : 0;
     li = active ? (int64_t)t.z : 0;
     code1 = t.y;
   } else {
-    active = dd < (A.rel_only ? R_ : ndest);
+    active = ws_ok && dd < (A.rel_only ? R_ : ndest);
     d = dd < R_ ? E_ + dd : dd - R_;
     li = d;
   }
@@ -825,7 +972,12 @@ void update_kernel(StepArgs A) {
     // issued together: the counter, the list's first 64 entries (speculative;
     // lanes past the count are ignored) and the entity row
     const uint32_t n = A.compact ? (uint32_t)A.htab[li] : A.cnt[d];
-    const uint32_t code0 = lst[min(lane, A.cap - 1)];
+    // list entry q (compact launches: position 0 is the leader's code1, and
+    // the list is read only once the count says there is more than one key)
+    const bool l0 = KGE_COMPACT_LIST0 && A.compact;
+    auto lst_at = [&](uint32_t q) -> uint32_t { return (l0 && q == 0u) ? code1 : lst[q]; };
+    uint32_t code0 = 0xFFFFFFFFu;
+    if (!A.compact) code0 = lst[min(lane, A.cap - 1)];   // speculative: issued with the counter
     F E, acc;
     acc.zero();
     E.zero();
@@ -929,6 +1081,7 @@ void update_kernel(StepArgs A) {
       } else if (n <= (uint32_t)A.cap && n <= (uint32_t)KGE_WAVE) {
         // ascending code order: each code's rank among the n (codes are
         // unique), then a forward permute puts code of rank r in lane r
+        if (A.compact) code0 = lane < (int)n ? lst_at((uint32_t)lane) : 0xFFFFFFFFu;
         const uint32_t code = lane < (int)n ? code0 : 0xFFFFFFFFu;
         uint32_t rank = 0u;
         for (int q = 0; q < (int)n; ++q) rank += ((uint32_t)__builtin_amdgcn_readlane((int)code, q) < code) ? 1u : 0u;
@@ -940,7 +1093,7 @@ void update_kernel(StepArgs A) {
 #pragma unroll
         for (int c = 0; c < CHMAX; ++c) {
           const uint32_t q = (uint32_t)(c * KGE_WAVE + lane);
-          code[c] = (c < nch && q < n) ? lst[q] : 0xFFFFFFFFu;
+          code[c] = (c < nch && q < n) ? lst_at(q) : 0xFFFFFFFFu;
         }
         uint32_t rank[CHMAX] = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -969,7 +1122,7 @@ void update_kernel(StepArgs A) {
         // a wave-local bitonic sort -- linear gather, n log^2 n compares
         uint32_t* buf = s_sort[wv];
         const uint32_t nl = min(n, (uint32_t)A.cap);
-        for (uint32_t q = lane; q < nl; q += KGE_WAVE) buf[q] = lst[q];
+        for (uint32_t q = lane; q < nl; q += KGE_WAVE) buf[q] = lst_at(q);
         if (n > nl) {
           const uint32_t novf = A.ctl->ovf_len;
           uint32_t fill = nl;
@@ -1013,7 +1166,7 @@ void update_kernel(StepArgs A) {
         for (uint32_t p = 0; p < n; ++p) {
           uint32_t best = 0xFFFFFFFFu;
           for (uint32_t q = lane; q < nl; q += KGE_WAVE) {
-            const uint32_t x = lst[q];
+            const uint32_t x = lst_at(q);
             if ((p == 0u || x > last) && x < best) best = x;
           }
           for (uint32_t q = lane; q < novf; q += KGE_WAVE) {

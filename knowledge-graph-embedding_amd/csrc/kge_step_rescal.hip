@@ -38,13 +38,13 @@ __global__ __launch_bounds__(256) void partials_norm_kernel(const float* part, i
   }
 }
 
-// RESCAL: context pass -> score (dot products against u / v) -> regulariser
-// loss -> projection + dR pass -> update kernel (dense entity gradient)
+// RESCAL: relation rank -> score (its waves form u = R^T h, v = R t, stream
+// the negatives as dot products against them, then g_h = R A, g_t = R^T B)
+// -> regulariser loss -> dR pass -> update kernel (dense entity gradient)
 template <int VEC, int NC>
 static kge_status rescal_vn(const StepArgs& A, const StepGeom& G, const RelArgs& P, float lam, float* regpart,
                             hipStream_t st, hipEvent_t const* ev) {
-  launch_rel_rank(P, st);
-  launch_rel_ctx(P, st);
+  if (A.train) launch_rel_rank(P, st);   // (the dR pass's relation groups)
   launch_score<Rescal, VEC, NC, SK_DOT>(A, G, st);
   // train steps fold the regulariser loss into passes that read every row
   // anyway (rel_dr: each R_r; the dense update: each entity row)

@@ -804,9 +804,11 @@ def test_fused_adam_three_steps(hiplib, model_name, constraint):
             np.testing.assert_allclose(got["v"].cpu().numpy(), vs, atol=TOL, err_msg="v %s step %d" % (kk, it + 1))
 
 
-@pytest.mark.parametrize("mode", ["sparse", "dense", "local"])
-@pytest.mark.parametrize("model_name,score_kind", [("TransE", "lp2"), ("TransD", "lppow2"), ("RotatE", "lp1"),
-                                                   ("TransR", "lppow2"), ("DistMult", None)])
+@pytest.mark.parametrize("mode,model_name,score_kind",
+                         [(m, n, s) for m in ("sparse", "dense", "local")
+                          for n, s in (("TransE", "lp2"), ("TransD", "lppow2"), ("RotatE", "lp1"),
+                                       ("TransR", "lppow2"), ("DistMult", None))]
+                         + [("dense", "RESCAL", None), ("dense", "TransH", "lppow2")])
 def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
     """KGE/sharded.py on the RCCL backend (world size 1): e mod G shard,
     kge_sample draws, the sparse (unique ids -> all_to_all ids / rows -> row

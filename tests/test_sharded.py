@@ -32,12 +32,14 @@ def _model(name, W, loss):
     from KGE import loss as L
     from KGE import score
     from KGE.models.semantic_based.DistMult import DistMult
+    from KGE.models.semantic_based.RESCAL import RESCAL
     from KGE.models.translating_based.RotatE import RotatE
+    from KGE.models.translating_based.TransH import TransH
     from KGE.models.translating_based.TransD import TransD
     from KGE.models.translating_based.TransE import TransE
     from KGE.ns_strategy import UniformStrategy
     lf = {"sans": L.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), "hinge": L.PairwiseHingeLoss(1.0),
-          "bce": L.BinaryCrossEntropyLoss()}[loss]
+          "bce": L.BinaryCrossEntropyLoss(), "sqerr": L.SquareErrorLoss()}[loss]
     ns = UniformStrategy(np.arange(E), seed=1)
     if name == "TransE":
         m = TransE({"embedding_size": D}, K, "h+t", score_fn=score.LpDistance(2), loss_fn=lf, ns_strategy=ns,
@@ -48,6 +50,12 @@ def _model(name, W, loss):
     elif name == "RotatE":
         m = RotatE({"embedding_size": D}, K, "h+t", score_fn=score.LpDistance(1), loss_fn=lf, ns_strategy=ns)
         m.limit = 0.7
+    elif name == "RESCAL":
+        m = RESCAL({"embedding_size": D}, K, "h+t", loss_fn=lf, ns_strategy=ns, constraint=True,
+                   constraint_weight=0.1)
+    elif name == "TransH":
+        m = TransH({"embedding_size": D}, K, "h+t", score_fn=score.LpDistancePow(2), loss_fn=lf, ns_strategy=ns,
+                   constraint=True, constraint_weight=0.1)
     else:
         m = DistMult({"embedding_size": D}, K, "h+t", loss_fn=lf, ns_strategy=ns, constraint=True,
                      constraint_weight=0.1)
@@ -63,6 +71,11 @@ def _case(seed, name):
              "ent_proj": rng.uniform(-0.5, 0.5, (E, D)), "rel_proj": rng.uniform(-0.5, 0.5, (R, 6))}
     elif name == "RotatE":
         W = {"ent_emb": rng.uniform(-0.5, 0.5, (E, D, 2)), "rel_emb": rng.uniform(-0.5, 0.5, (R, D))}
+    elif name == "RESCAL":
+        W = {"ent_emb": rng.uniform(-0.5, 0.5, (E, D)), "rel_inter": rng.uniform(-0.3, 0.3, (R, D, D))}
+    elif name == "TransH":
+        W = {"ent_emb": rng.uniform(-0.5, 0.5, (E, D)), "rel_emb": rng.uniform(-0.5, 0.5, (R, D)),
+             "rel_hyper": rng.uniform(-0.5, 0.5, (R, D))}
     else:
         rk = "rel_emb" if name == "TransE" else "rel_inter"
         W = {"ent_emb": rng.uniform(-0.5, 0.5, (E, D)), rk: rng.uniform(-0.5, 0.5, (R, D))}
@@ -83,6 +96,7 @@ def _worker(rank, port, name, loss, opt, steps, mode, out):
     assert st.valid == len(range(rank, E, 2))
     if mode == "dense":
         assert not hasattr(st, "shard") and len(st.gent) == (2 if name == "TransD" else 1)
+    assert st.mode == mode
     o = optimizers.SGD(0.05) if opt == "sgd" else optimizers.Adam(0.01)
     for s in range(steps):
         b = torch.tensor(pos[rank * B:(rank + 1) * B])
@@ -127,6 +141,46 @@ def test_sharded_sgd_equals_single_device_oracle(name, loss, mode):
     assert abs(got_loss - ref["loss"]) <= 1e-5 * max(1.0, abs(ref["loss"]))
     for k, v in ref["weights"].items():
         np.testing.assert_allclose(got[k], v, atol=2e-6, err_msg=k)
+
+
+@pytest.mark.parametrize("name,loss", [("RESCAL", "sqerr"), ("TransH", "sans"), ("TransH", "hinge")])
+@pytest.mark.parametrize("opt", ["sgd", "adam"])
+def test_sharded_full_table_regulariser_dense_mode(name, loss, opt):
+    """RESCAL / TransH with constraint (dense gradients of every row,
+    RESCAL.py:190-198, TransH.py:202-211) across 2 ranks in the dense
+    exchange: each rank adds half of the regulariser, the all-reduce sums it,
+    the clip norm is the reduced tensor's -- two steps == two single-device
+    steps at 2B (oracle for SGD, the eager path for Adam)."""
+    got, got_loss = _run(name, loss, opt, 2, "dense")
+    W, pos, neg = _case(0, name)
+    spec = {"sans": ("sans", 3.0, 1.0), "hinge": ("hinge", 1.0), "sqerr": ("sqerr",)}[loss]
+    sc = {"RESCAL": ("dot", 0.0), "TransH": ("lppow", 2.0)}[name]
+    ref_w, state = W, None
+    for _ in range(2):
+        ref = orc.train_step(name, ref_w, pos, neg, score=sc, loss=spec, lr=0.05 if opt == "sgd" else 0.01,
+                             constraint=True, constraint_weight=0.1, side="h+t", optimizer=opt, adam_state=state)
+        ref_w, state = ref["weights"], ref.get("adam")
+    assert abs(got_loss - ref["loss"]) <= 1e-5 * max(1.0, abs(ref["loss"]))
+    for k, v in ref_w.items():
+        np.testing.assert_allclose(got[k], v, atol=2e-6, err_msg=k)
+
+
+def test_sparse_mode_refuses_full_table_regulariser():
+    os.environ["KGE_BACKEND"] = "eager"
+    try:
+        import torch.distributed as dist
+        from KGE.sharded import ShardedStep
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % _port(), rank=0, world_size=1)
+        try:
+            W, _, _ = _case(0, "RESCAL")
+            m = _model("RESCAL", W, "sqerr")
+            assert ShardedStep(m).mode == "dense"   # auto picks the dense exchange at any size
+            with pytest.raises(NotImplementedError):
+                ShardedStep(m, mode="sparse")
+        finally:
+            dist.destroy_process_group()
+    finally:
+        os.environ.pop("KGE_BACKEND", None)
 
 
 @pytest.mark.parametrize("mode", ["sparse", "dense"])
