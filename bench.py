@@ -376,7 +376,7 @@ def train_leg(args, dev):
     meta = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
     model = TransE({"embedding_size": d}, K, w["side"], score_fn=w["score"], loss_fn=w["loss"],
                    ns_strategy=UniformStrategy, constraint=w["constraint"])
-    per_epoch = {"histogram": 0.0, "checkpoint": 0.0}
+    per_epoch = {"histogram": 0.0, "checkpoint": 0.0, "batch_host": 0.0}
 
     def timed(name, fn):
         def run(*a, **k):
@@ -387,6 +387,8 @@ def train_leg(args, dev):
         return run
     model._log_embeddings_histogram = timed("histogram", model._log_embeddings_histogram)
     model._save_checkpoint = timed("checkpoint", model._save_checkpoint)
+    # host time spent issuing each batch (no sync inside: the GPU runs behind)
+    model._run_single_batch = timed("batch_host", model._run_single_batch)
     nb = int(math.ceil(len(triples) / B))
     with tempfile.TemporaryDirectory() as logdir:
         model.train(train_X=triples, val_X=None, metadata=meta, epochs=1, batch_size=B,
@@ -426,6 +428,7 @@ def train_leg(args, dev):
                       "epochs": args.epochs, "batches_per_epoch": nb, "global_batch": B, "negatives": K, "dim": d,
                       "parallelism": "dp1"},
            "train_entry": {"ms_per_batch_wall": round(ms, 5), "ms_per_batch_loop": round(loop_ms, 5),
+                           "host_issue_ms_per_batch": round(per_epoch["batch_host"] * 1e3 / steps, 5),
                            "fused_step_ms": round(fused_ms, 5),
                            "host_overhead_ms_per_batch": round(loop_ms - fused_ms, 5),
                            "per_epoch_ms": {"histogram": round(hist_ms, 3), "checkpoint": round(ckpt_ms, 3)}},

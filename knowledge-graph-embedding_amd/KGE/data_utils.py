@@ -144,7 +144,11 @@ class DeviceBatcher:
     reproducible (TF is not installed); the stream semantics are.
     """
 
-    def __init__(self, data, batch_size, shuffle, seed=None, device=None):
+    def __init__(self, data, batch_size, shuffle, seed=None, device=None, reuse_buffer=False):
+        """``reuse_buffer``: every batch is written into the same device buffer
+        (the caller consumes a batch before drawing the next -- the training
+        loop; stream order makes the overwrite safe), saving an allocation
+        per batch."""
         host = load_triples(data)
         if host.dtype not in (torch.int32, torch.int64):
             host = host.to(torch.int64)
@@ -160,6 +164,9 @@ class DeviceBatcher:
         self.seed = int(seed) if seed is not None else int.from_bytes(os.urandom(8), "little")
         self.seed &= (1 << 64) - 1
         self._pos = 0   # stream position of the next batch's first row
+        self.reuse_buffer = bool(reuse_buffer)
+        self._desc = None
+        self._out = None
 
     def __iter__(self):
         return self
@@ -176,26 +183,35 @@ class DeviceBatcher:
             import ctypes
             from . import _hip
             L = _hip.load()
-            out = torch.empty((B, 3), dtype=self.data.dtype, device=self.data.device)
-            d = _hip.kge_stream_desc()
-            d.abi_version = _hip.ABI_VERSION
-            d.idx_dtype = _hip.IDX_I64 if self.data.dtype == torch.int64 else _hip.IDX_I32
-            d.triples = self.data.data_ptr()
-            d.n_rows = self.n
+            if self.reuse_buffer and self._out is not None:
+                out = self._out
+            else:
+                out = torch.empty((B, 3), dtype=self.data.dtype, device=self.data.device)
+                if self.reuse_buffer:
+                    self._out = out
+            d = self._desc
+            if d is None:   # the descriptor is built once; a batch changes start and out
+                d = _hip.kge_stream_desc()
+                d.abi_version = _hip.ABI_VERSION
+                d.idx_dtype = _hip.IDX_I64 if self.data.dtype == torch.int64 else _hip.IDX_I32
+                d.triples = self.data.data_ptr()
+                d.n_rows = self.n
+                d.batch = B
+                d.seed = self.seed
+                d.shuffle = 1 if self.shuffle else 0
+                self._desc = d
+                self._dref = ctypes.byref(d)
             d.start = start
-            d.batch = B
-            d.seed = self.seed
-            d.shuffle = 1 if self.shuffle else 0
             d.out = out.data_ptr()
             stream = torch.cuda.current_stream(self.data.device).cuda_stream
-            _hip.check(L.kge_stream_batch(ctypes.byref(d), ctypes.c_void_p(stream)), "kge_stream_batch")
+            _hip.check(L.kge_stream_batch(self._dref, ctypes.c_void_p(stream)), "kge_stream_batch")
             return out
         idx = torch.from_numpy(self.rows(start, B))
         return self.data.index_select(0, idx)
 
 
-def set_tf_iterator(data, batch_size, shuffle, buffer_size=None, seed=None, device=None):
+def set_tf_iterator(data, batch_size, shuffle, buffer_size=None, seed=None, device=None, reuse_buffer=False):
     """Drop-in for ``set_tf_iterator`` (``data_utils.py:176-196``)."""
     if shuffle:
         assert buffer_size is not None, "buffer_size must be given when shuffle is True"
-    return DeviceBatcher(data, batch_size, shuffle, seed=seed, device=device)
+    return DeviceBatcher(data, batch_size, shuffle, seed=seed, device=device, reuse_buffer=reuse_buffer)

@@ -255,7 +255,10 @@ class FusedStep:
         return d
 
     def __call__(self, batch, is_train, optimizer, neg_ids=None, pos_score=None, neg_score=None,
-                 prof_events=None):
+                 prof_events=None, accum=None):
+        """One step; ``accum`` (device float32 [1], optional) receives += the
+        batch loss inside the step (the training loop's per-epoch sum: no
+        per-batch host work), else the step's own ``loss_accum``."""
         if batch.device != self.device:
             batch = batch.to(self.device)
         if batch.dtype not in (torch.int32, torch.int64):
@@ -303,6 +306,7 @@ class FusedStep:
             d.workspace_bytes = self.workspace.numel()
             self._cache = (key, d)
         d.prof_events = ctypes.cast(prof_events, ctypes.c_void_p) if prof_events is not None else None
+        d.loss_accum = (accum if accum is not None else self.loss_accum).data_ptr()
         _hip.check(self.lib.kge_step(d, _hip.stream_handle(self.device)), "kge_step")
         if is_train and isinstance(optimizer, _opt.Adam) and not self.grad_mode:
             self.apply_adam(optimizer)

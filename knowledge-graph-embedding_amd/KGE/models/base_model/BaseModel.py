@@ -98,12 +98,15 @@ class KGEModel:
 
         logging.info("[%s] Start Training..." % str(datetime.datetime.now()))
         for i in range(epochs):
-            train_loss = torch.zeros((), dtype=torch.float64, device=self._device)
-            val_loss = torch.zeros((), dtype=torch.float64, device=self._device)
+            # per-epoch loss sums stay on the device: the fused step adds each
+            # batch's loss into them itself (no per-batch host work); the host
+            # reads them once per epoch (the reference syncs every batch, :330)
+            train_loss = torch.zeros(1, dtype=torch.float32, device=self._device)
+            val_loss = torch.zeros(1, dtype=torch.float32, device=self._device)
             for b in range(self._batch_count_train):
-                train_loss += self._run_single_batch(next(train_iter), is_train=True)
+                self._run_single_batch(next(train_iter), is_train=True, accum=train_loss)
                 if val_iter is not None and b < self._batch_count_val:
-                    val_loss += self._run_single_batch(next(val_iter), is_train=False)
+                    self._run_single_batch(next(val_iter), is_train=False, accum=val_loss)
             self._check_device_status()
             train_loss = float(train_loss) / self._batch_count_train
             train_loss_history.append(train_loss)
@@ -141,11 +144,11 @@ class KGEModel:
         n_train = calculate_data_size(train_X)
         self._batch_count_train = int(np.ceil(n_train / self.batch_size))
         train_iter = set_tf_iterator(train_X, self.batch_size, shuffle=True, buffer_size=n_train,
-                                     seed=self.seed, device=self._device)
+                                     seed=self.seed, device=self._device, reuse_buffer=True)
         if val_X is not None:
             n_val = calculate_data_size(val_X)
             self._batch_count_val = int(np.ceil(n_val / self.batch_size))
-            val_iter = set_tf_iterator(val_X, self.batch_size, shuffle=False, device=self._device)
+            val_iter = set_tf_iterator(val_X, self.batch_size, shuffle=False, device=self._device, reuse_buffer=True)
         else:
             self._batch_count_val = 0
             val_iter = None
@@ -178,11 +181,23 @@ class KGEModel:
             self.model_weights[k] = w.detach().to(device=dev, dtype=torch.float32).contiguous()
 
     # ------------------------------------------------------------ step
-    def _run_single_batch(self, batch_data, is_train):
-        """One batch (``BaseModel.py:293-330``); returns the loss as a device scalar."""
+    def _plan_for(self, opt, batch_size):
+        """engine.fused_plan, cached per (optimizer, batch size, plugins)."""
+        key = (id(opt), batch_size, id(getattr(self, "score_fn", None)), id(self.loss_fn), id(self.ns_strategy),
+               self.negative_ratio, self.corrupt_side, bool(getattr(self, "constraint", False)), engine.backend(),
+               id(self.model_weights.get("ent_emb")))
+        c = self.__dict__.get("_plan_key")
+        if c is None or c[0] != key:
+            self._plan_key = (key, engine.fused_plan(self, opt, batch_size))
+        return self._plan_key[1]
+
+    def _run_single_batch(self, batch_data, is_train, accum=None):
+        """One batch (``BaseModel.py:293-330``). Returns the loss as a device
+        scalar, or, given ``accum`` (device float32 [1]), adds it there and
+        returns None (the fused single-device step adds it in-kernel)."""
         opt = self._optimizer if is_train else None
         world = _world_size()
-        reason = engine.fused_plan(self, opt, batch_data.shape[0] // world)
+        reason = self._plan_for(opt, batch_data.shape[0] // world)
         if reason is None:
             if self._fused is None:
                 if world > 1:
@@ -196,12 +211,23 @@ class KGEModel:
                 assert n % world == 0, "batch_size must be divisible by the world size"
                 rank = torch.distributed.get_rank()
                 batch_data = batch_data[rank * (n // world):(rank + 1) * (n // world)]
-            return self._fused(batch_data, is_train, opt).clone().reshape(()).to(torch.float64)
+            if accum is not None and isinstance(self._fused, engine.FusedStep):
+                self._fused(batch_data, is_train, opt, accum=accum)
+                return None
+            loss = self._fused(batch_data, is_train, opt)
+            if accum is not None:
+                accum += loss.reshape(1)     # (the multi-GPU loss is final only after its all-reduce)
+                return None
+            return loss.clone().reshape(()).to(torch.float64)
         if world > 1:
             raise NotImplementedError("multi-GPU training needs a fused combination (%s)" % reason)
         if engine.backend() != "eager":
             engine.warn_once((type(self).__name__, reason), "eager plugin path: %s" % reason)
-        return engine.eager_step(self, batch_data, is_train, opt).to(torch.float64)
+        loss = engine.eager_step(self, batch_data, is_train, opt)
+        if accum is not None:
+            accum += loss.reshape(1).to(accum.dtype)
+            return None
+        return loss.to(torch.float64)
 
     def sync_weights(self):
         """Multi-GPU: gather the entity shards into ``model_weights`` (before evaluation)."""

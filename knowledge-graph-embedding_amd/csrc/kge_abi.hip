@@ -685,22 +685,10 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   } else if (P.transr) {
     s = launch_step_transr(A, P.G, TA, RA, P.sk, st, ev);
   } else if (P.rescal) {
+    // (SGD: the dense applies are the chain's last launch, BaseModel.py:327-328)
+    RA.lazy_absent = d->optimizer == KGE_OPT_SGD && rescal_apply_fused_ok(RA, A.ent, A.gent);
     s = launch_step_rescal(A, P.G, RA, d->constraint ? d->constraint_weight : 0.f,
                            (float*)(ws + P.o_regpart), st, ev);
-    if (s == KGE_OK && d->optimizer == KGE_OPT_SGD) {
-      // keras SGD on the dense gradients: clip_by_norm with the dense norm^2
-      // the update / dR passes reduced (BaseModel.py:327-328)
-      const kge_table* tabs[2] = {&d->ent, &d->rel};
-      const float* gs[2] = {A.gent, RA.grel};
-      for (int v = 0; v < 2; ++v) {
-        const kge_table& t = *tabs[v];
-        ApplyArgs a{};
-        a.w = t.data; a.rows = t.rows; a.cols = (int32_t)t.cols; a.ld = t.ld;
-        a.g = gs[v]; a.norm2 = &A.ctl->dn2[v]; a.lr = d->lr; a.clip = d->clip_norm;
-        a.ctl = A.ctl; a.sig = A.sig; a.status = A.status;
-        launch_apply(a, st);
-      }
-    }
   } else {
     s = launch_step_elementwise(A, P.G, d->model, P.sk, st, ev);
   }

@@ -236,6 +236,7 @@ struct TransE {
   static constexpr bool CPLX = false;
   static constexpr bool WIDE = false;   // score kernel fits 128 VGPRs at one chunk (4 waves / SIMD)
   static constexpr bool SELF_CTX = false;   // context rows computed by the score kernel itself (RESCAL)
+  static constexpr bool FAST_STREAM = false;   // stream partial / gradient in hardware-rate forms (RotatE)
   static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
@@ -387,6 +388,7 @@ struct DistMult {
   static constexpr bool CPLX = false;
   static constexpr bool WIDE = true;    // five context rows: 256-VGPR budget (2 waves / SIMD)
   static constexpr bool SELF_CTX = false;
+  static constexpr bool FAST_STREAM = false;
   static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
@@ -470,6 +472,12 @@ struct RotatE {
   static constexpr bool CPLX = true;
   static constexpr bool WIDE = true;
   static constexpr bool SELF_CTX = false;
+  // C3's stream is VALU-bound on IEEE sqrt / divide per complex element
+  // (PMC: 41 % of wave cycles issuing VALU, ~90 instructions per element):
+  // LpDistance p = 1 / 2 stream rows use v_rsq once per element (|a| = s
+  // rsq(s) for the score, a rsq(s) for the gradient, kept from forward to
+  // backward in b); p = inf keeps the IEEE modulus (exact arg-max ties)
+  static constexpr bool FAST_STREAM = SK == SK_P1 || SK == SK_P2;
   static constexpr bool MAT = false;
   static constexpr int NSNAP = 3;
   static constexpr int HV = VEC / 2;
@@ -508,15 +516,53 @@ struct RotatE {
 #pragma unroll
     for (int i = 0; i < VEC * NC; ++i) a.v[i] = x.v[i] - y.v[i];
   }
+  // stream partial of a row (FAST_STREAM): b.v[2k] <- rsq(|a_k|^2) for bwdk
+  template <int SKK>
+  __device__ static float fast_partial(const F& a, F& b) {
+    float acc = 0.f;
+#pragma unroll
+    for (int i = 0; i < VEC * NC; i += 2) {
+      const float s = a.v[i] * a.v[i] + a.v[i + 1] * a.v[i + 1];
+      if (SKK == SK_P2) {
+        acc += s;
+      } else {
+        const float r = s > 0.f ? __builtin_amdgcn_rsqf(s) : 0.f;
+        b.v[i] = r;
+        acc += s * r;
+      }
+    }
+    return acc;
+  }
   // g_h = g_x * conj(w); g_theta = gxi * x_re - gxr * x_im
+  // (FAST: the stream rows' element gradients from fast_partial's rsq in b,
+  // and x of an h-corrupted row as a + t instead of a second complex product)
+  template <bool FAST = false>
   __device__ static void bwd(const Ctx& c, int kind, const F& E, const F& a, const F& b,
                              float alpha, float M, F& accH, F& accR, F& accT, float* nrm,
                              const MP& mp) {
-    const float limit = mp.limit;
+    const float plim = kPiF / mp.limit;
     F gx;
-    score_grad<SK, true>(a, alpha, M, gx);
+    if constexpr (FAST && SK == SK_P1) {
+#pragma unroll
+      for (int i = 0; i < VEC * NC; i += 2) {
+        const float s = alpha * b.v[i];
+        gx.v[i] = s * a.v[i];
+        gx.v[i + 1] = s * a.v[i + 1];
+      }
+    } else {
+      score_grad<SK, true>(a, alpha, M, gx);
+    }
     F x;
-    if (kind == KIND_HC) cmul(E, c.CS, x); else x = c.X;
+    if (kind == KIND_HC) {
+      if constexpr (FAST) {
+#pragma unroll
+        for (int i = 0; i < VEC * NC; ++i) x.v[i] = a.v[i] + c.T.v[i];
+      } else {
+        cmul(E, c.CS, x);
+      }
+    } else {
+      x = c.X;
+    }
     F gH;
     float gth2 = 0.f;
 #pragma unroll
@@ -525,7 +571,7 @@ struct RotatE {
       gH.v[i] = gx.v[i] * co + gx.v[i + 1] * si;
       gH.v[i + 1] = gx.v[i + 1] * co - gx.v[i] * si;
       const float gth = gx.v[i + 1] * x.v[i] - gx.v[i] * x.v[i + 1];
-      const float gr = (gth * kPiF) / limit;
+      const float gr = gth * plim;
       accR.v[i] += gr;   // phase gradient kept in the even slot
       gth2 += gr * gr;
     }
@@ -545,7 +591,7 @@ struct RotatE {
   template <int KIND>
   __device__ static void bwdk(const Ctx& c, const F& E, const F& a, const F& b, float alpha, float M,
                               F& accH, F& accR, F& accT, float* nrm, const MP& mp) {
-    bwd(c, KIND, E, a, b, alpha, M, accH, accR, accT, nrm, mp);
+    bwd<FAST_STREAM>(c, KIND, E, a, b, alpha, M, accH, accR, accT, nrm, mp);
   }
   __device__ static void finish(F& accH, F& accR, F& accT) {}
   __device__ static void write_snap(const Ctx& c, float* sb, int cols) {
@@ -560,12 +606,27 @@ struct RotatE {
     load_row(ec.c0, sb + (kind == KIND_TC ? 0 : cols), cols);
     load_row(ec.c1, sb + 2 * cols, cols);
   }
+  // element gradient of a row's score (the update kernel's re-derivation):
+  // p = 1 with the stream's v_rsq form, else score_grad
+  __device__ static void row_grad(const F& a, float alpha, float M, F& g) {
+    if constexpr (SK == SK_P1) {
+#pragma unroll
+      for (int i = 0; i < VEC * NC; i += 2) {
+        const float s = a.v[i] * a.v[i] + a.v[i + 1] * a.v[i + 1];
+        const float k = s > 0.f ? alpha * __builtin_amdgcn_rsqf(s) : 0.f;
+        g.v[i] = k * a.v[i];
+        g.v[i + 1] = k * a.v[i + 1];
+      }
+    } else {
+      score_grad<SK, true>(a, alpha, M, g);
+    }
+  }
   __device__ static void grad_entity(const ECtx& ec, int kind, const F& E, float alpha, float M, F& gE) {
     if (kind == KIND_TC) {
       F a, g;
 #pragma unroll
       for (int i = 0; i < VEC * NC; ++i) a.v[i] = ec.c0.v[i] - E.v[i];
-      score_grad<SK, true>(a, alpha, M, g);
+      row_grad(a, alpha, M, g);
 #pragma unroll
       for (int i = 0; i < VEC * NC; ++i) gE.v[i] = -g.v[i];
     } else {
@@ -573,7 +634,7 @@ struct RotatE {
       cmul(E, ec.c0, x);
 #pragma unroll
       for (int i = 0; i < VEC * NC; ++i) a.v[i] = x.v[i] - ec.c1.v[i];
-      score_grad<SK, true>(a, alpha, M, g);
+      row_grad(a, alpha, M, g);
 #pragma unroll
       for (int i = 0; i < VEC * NC; i += 2) {
         const float co = ec.c0.v[i], si = ec.c0.v[i + 1];
@@ -606,6 +667,7 @@ struct Rescal {
   // u = R^T h, v = R t computed by the positive's own score waves (and the
   // post products g_h = R A, g_t = R^T B after the merge): no separate passes
   static constexpr bool SELF_CTX = true;
+  static constexpr bool FAST_STREAM = false;
   static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;
   using F = Frag<VEC, NC>;
@@ -675,6 +737,7 @@ struct Materialised {
   static constexpr bool CPLX = false;
   static constexpr bool WIDE = false;
   static constexpr bool SELF_CTX = false;
+  static constexpr bool FAST_STREAM = false;
   static constexpr bool MAT = true;
   static constexpr int NSNAP = 0;
   static constexpr bool NRM_FROM_R = false;

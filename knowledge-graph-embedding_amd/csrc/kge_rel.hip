@@ -196,19 +196,24 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
     }
   }
   // epilogue: the accumulators go through LDS and the run is written a float4
-  // per lane (most workgroups -- relations absent from the batch -- do
-  // nothing else: their strip is dense_rel * R_r)
+  // per lane. Relations absent from the batch (most workgroups) have no
+  // MFMA part: their strip is dense_rel * R_r -- not even written when the
+  // apply pass re-derives it (lazy_absent: the norm partials only)
+  const bool absent = beg == end;
+  const bool store = !(absent && P.lazy_absent);
   float* G = P.grel + r * (int64_t)d * d + (int64_t)i0 * d;
   float* S = Yc;   // [16][D16]
-  __syncthreads();   // the MFMA loop's last reads of Yc
+  if (!absent) {
+    __syncthreads();   // the MFMA loop's last reads of Yc
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int jt = wv + 4 * t;
-    if (jt >= nct) continue;
+    for (int t = 0; t < 4; ++t) {
+      const int jt = wv + 4 * t;
+      if (jt >= nct) continue;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) S[((lane >> 4) * 4 + g) * D16 + jt * 16 + (lane & 15)] = acc[t][g];
+      for (int g = 0; g < 4; ++g) S[((lane >> 4) * 4 + g) * D16 + jt * 16 + (lane & 15)] = acc[t][g];
+    }
+    __syncthreads();
   }
-  __syncthreads();
   float n2 = 0.f, m2 = 0.f;   // gradient norm^2 | ||R_r||^2 (regulariser loss)
   if (v4) {
 #pragma unroll
@@ -216,13 +221,15 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
       const int e = 4 * (threadIdx.x + k * 256);
       if (e >= run) continue;
       const int row = e / d, col = e - row * d;
-      const float* sv = S + row * D16 + col;
+      float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!absent) sv = make_float4(S[row * D16 + col], S[row * D16 + col + 1], S[row * D16 + col + 2],
+                                    S[row * D16 + col + 3]);
       float4 v;
-      v.x = sv[0] + P.dense_rel * m[k].x;
-      v.y = sv[1] + P.dense_rel * m[k].y;
-      v.z = sv[2] + P.dense_rel * m[k].z;
-      v.w = sv[3] + P.dense_rel * m[k].w;
-      *reinterpret_cast<float4*>(G + e) = v;
+      v.x = sv.x + P.dense_rel * m[k].x;
+      v.y = sv.y + P.dense_rel * m[k].y;
+      v.z = sv.z + P.dense_rel * m[k].z;
+      v.w = sv.w + P.dense_rel * m[k].w;
+      if (store) *reinterpret_cast<float4*>(G + e) = v;
       n2 += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
       m2 += m[k].x * m[k].x + m[k].y * m[k].y + m[k].z * m[k].z + m[k].w * m[k].w;
     }
@@ -230,7 +237,7 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
     for (int e = threadIdx.x; e < run; e += blockDim.x) {
       const int row = e / d, col = e - row * d;
       const float rm = Rm[e];
-      const float v = S[row * D16 + col] + P.dense_rel * rm;
+      const float v = (absent ? 0.f : S[row * D16 + col]) + P.dense_rel * rm;
       G[e] = v;
       n2 += v * v;
       m2 += rm * rm;
@@ -241,34 +248,97 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
   if (lane == 0) { s_n2[wv] = n2; s_m2[wv] = m2; }
   __syncthreads();
   // the strip's partials ([grid] gradient norm^2 | [grid] ||R||^2);
-  // rel_dr_norm_kernel (next launch on the stream) sums them in a fixed
+  // rescal_norms_kernel (after the dense entity update) sums them in a fixed
   // order -- no grid-wide ticket: 3 k workgroups taking turns on one counter
-  // cost more than the extra launch
+  // cost more than a one-workgroup launch
   if (threadIdx.x < 2) {
     const float* q = threadIdx.x ? s_m2 : s_n2;
     P.rpart[threadIdx.x * gridDim.x + blockIdx.x] = q[0] + q[1] + q[2] + q[3];
   }
 }
 
-__global__ __launch_bounds__(256) void rel_dr_norm_kernel(RelArgs P, int n) {
+// RESCAL train step, after the dR pass and the dense entity update: one
+// workgroup sums both passes' partials in a fixed order -- the dense
+// gradients' norm^2 (clip_by_norm of each dense tensor), ||R||^2 and ||e||^2
+// for the regulariser loss lambda (mean_e ||e||^2 + mean_r ||R_r||_F^2)
+// (RESCAL.py:190-198) -- and publishes the two SGD scales for the apply.
+__global__ __launch_bounds__(256) void rescal_norms_kernel(RelArgs P, int nr, const float* upart, int nu, float lam,
+                                                           float lr, float clip, float* loss_accum) {
   if (ws_refused(P.ctl, P.sig, P.status, P.loss_out)) return;
-  __shared__ float s_n2[4], s_m2[4];
+  __shared__ float s_w[4][4];
   const int lane = lane_id(), wv = wave_id();
-  float s = 0.f, m = 0.f;
-  for (int w = threadIdx.x; w < n; w += blockDim.x) {
-    s += P.rpart[w];
-    m += P.rpart[n + w];
+  float a[4] = {0.f, 0.f, 0.f, 0.f};   // rel grad^2 | ||R||^2 | ent grad^2 | ||e||^2
+  for (int w = threadIdx.x; w < nr; w += blockDim.x) {
+    a[0] += P.rpart[w];
+    a[1] += P.rpart[nr + w];
   }
-  s = wave_sum(s);
-  m = wave_sum(m);
-  if (lane == 0) { s_n2[wv] = s; s_m2[wv] = m; }
+  for (int w = threadIdx.x; w < nu; w += blockDim.x) {
+    a[2] += upart[w];
+    a[3] += upart[nu + w];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) a[k] = wave_sum(a[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s_w[wv][k] = a[k];
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float t = s_n2[0] + s_n2[1] + s_n2[2] + s_n2[3];
-    P.ctl->dn2[1] = t;
-    P.ctl->reg_r2 = s_m2[0] + s_m2[1] + s_m2[2] + s_m2[3];
-    if (P.norm2_out) P.norm2_out[1] = t;
+    float t[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] = s_w[0][k] + s_w[1][k] + s_w[2][k] + s_w[3][k];
+    P.ctl->dn2[0] = t[2];
+    P.ctl->dn2[1] = t[0];
+    P.ctl->reg_r2 = t[1];
+    P.ctl->scale[0] = -lr * (clip / fmaxf(sqrtf(t[2]), clip));
+    P.ctl->scale[1] = -lr * (clip / fmaxf(sqrtf(t[0]), clip));
+    if (P.norm2_out) { P.norm2_out[0] = t[2]; P.norm2_out[1] = t[0]; }
+    if (lam != 0.f) {
+      const float add = lam * (t[3] / (float)P.ent.rows + t[1] / (float)P.rel.rows);
+      P.loss_out[0] += add;
+      if (loss_accum) loss_accum[0] += add;
+    }
   }
+}
+
+// RESCAL in-step SGD of both dense gradients in one launch (keras SGD after
+// clip_by_norm, BaseModel.py:327-328): blocks [0, be) stream the entity
+// table a float4 per thread (w + (g * cs) * -lr), the rest go relation by
+// relation over 1024-float chunks of R_r -- a relation absent from the batch
+// has the gradient dense_rel * R_r, re-derived here (the dR pass wrote none
+// of it), the same arithmetic as when it is stored.
+__global__ __launch_bounds__(256) void rescal_apply_kernel(RelArgs P, float* ent, const float* gent, int64_t n4e,
+                                                           int64_t be, int64_t bpr, float lr, float clip) {
+  if (ws_refused(P.ctl, P.sig, P.status, P.loss_out)) return;
+  if ((int64_t)blockIdx.x < be) {
+    const float cs = clip / fmaxf(sqrtf(P.ctl->dn2[0]), clip);
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= n4e) return;
+    float4 w = reinterpret_cast<float4*>(ent)[q];
+    const float4 g = reinterpret_cast<const float4*>(gent)[q];
+    w.x = w.x + (g.x * cs) * (-lr); w.y = w.y + (g.y * cs) * (-lr);
+    w.z = w.z + (g.z * cs) * (-lr); w.w = w.w + (g.w * cs) * (-lr);
+    reinterpret_cast<float4*>(ent)[q] = w;
+    return;
+  }
+  const int64_t b = blockIdx.x - be;
+  const int64_t r = b / bpr, ch = b - r * bpr;
+  const int64_t dd = (int64_t)P.d * P.d;
+  const int64_t e = ch * 1024 + 4 * threadIdx.x;
+  if (e >= dd) return;
+  const float cs = clip / fmaxf(sqrtf(P.ctl->dn2[1]), clip);
+  float4* wp = reinterpret_cast<float4*>(P.rel.p + r * P.rel.ld + e);
+  float4 w = *wp;
+  float4 g;
+  if (P.rel_cnt[r] == 0) {
+    g.x = 0.f + P.dense_rel * w.x; g.y = 0.f + P.dense_rel * w.y;
+    g.z = 0.f + P.dense_rel * w.z; g.w = 0.f + P.dense_rel * w.w;
+  } else {
+    g = *reinterpret_cast<const float4*>(P.grel + r * dd + e);
+  }
+  w.x = w.x + (g.x * cs) * (-lr); w.y = w.y + (g.y * cs) * (-lr);
+  w.z = w.z + (g.z * cs) * (-lr); w.w = w.w + (g.w * cs) * (-lr);
+  *wp = w;
 }
 
 // ------------------------------------------------------------ KL regulariser loss
@@ -365,12 +435,31 @@ void launch_rel_rank(const RelArgs& P, hipStream_t st) {
   else
     hipLaunchKernelGGL(rel_rank_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P);
 }
+void launch_rescal_norms(const RelArgs& P, const float* upart, int nu, float lam, float lr, float clip,
+                         float* loss_accum, hipStream_t st) {
+  const int nct = (P.d + 15) / 16;
+  hipLaunchKernelGGL(rescal_norms_kernel, dim3(1), dim3(256), 0, st, P, (int)(P.rel.rows * nct), upart, nu, lam, lr,
+                     clip, loss_accum);
+}
+bool rescal_apply_fused_ok(const RelArgs& P, const TabView& ent, const float* gent) {
+  const int64_t dd = (int64_t)P.d * P.d;
+  return dd % 4 == 0 && P.rel.ld % 4 == 0 && ((uintptr_t)P.rel.p % 16) == 0 && ((uintptr_t)P.grel % 16) == 0 &&
+         ent.ld == ent.cols && ((int64_t)ent.rows * ent.cols) % 4 == 0 && ((uintptr_t)ent.p % 16) == 0 &&
+         ((uintptr_t)gent % 16) == 0;
+}
+void launch_rescal_apply(const RelArgs& P, const TabView& ent, const float* gent, float lr, float clip,
+                         hipStream_t st) {
+  const int64_t n4e = ent.rows * (int64_t)ent.cols / 4;
+  const int64_t be = (n4e + 255) / 256;
+  const int64_t bpr = ((int64_t)P.d * P.d + 1023) / 1024;
+  hipLaunchKernelGGL(rescal_apply_kernel, dim3((unsigned)(be + P.rel.rows * bpr)), dim3(256), 0, st, P, ent.p, gent,
+                     n4e, be, bpr, lr, clip);
+}
 void launch_rel_post(const RelArgs& P, hipStream_t st) {
   // (g_h, g_t: the score kernel's waves, Rescal::SELF_CTX)
   const int nct = (P.d + 15) / 16;
   const size_t lds2 = (32 * 16 + 16 * (size_t)nct * 16) * sizeof(float);
   hipLaunchKernelGGL(rel_dr_kernel, dim3((unsigned)(P.rel.rows * nct)), dim3(256), lds2, st, P);
-  hipLaunchKernelGGL(rel_dr_norm_kernel, dim3(1), dim3(256), 0, st, P, (int)(P.rel.rows * nct));
 }
 void launch_reg_loss(const TabView& ent, const TabView& rel, float lam, float* part, StepCtl* ctl,
                      float* loss_out, float* loss_accum, uint32_t sig, int32_t* status, hipStream_t st) {

@@ -224,9 +224,16 @@ struct RelArgs {
   int32_t* status;
   uint32_t sig;              // plan signature (ws_refused)
   float* loss_out;
+  bool lazy_absent;          // SGD step: absent relations' dense gradient re-derived by the apply (not stored)
 };
 void launch_rel_rank(const RelArgs& R, hipStream_t st);
-void launch_rel_post(const RelArgs& R, hipStream_t st);     // dR (+ dense term, norm^2)
+void launch_rel_post(const RelArgs& R, hipStream_t st);     // dR (+ dense term, norm^2 partials)
+// train step tail: both passes' norms + the loss term, then both SGD applies in one launch
+void launch_rescal_norms(const RelArgs& P, const float* upart, int nu, float lam, float lr, float clip,
+                         float* loss_accum, hipStream_t st);
+bool rescal_apply_fused_ok(const RelArgs& P, const TabView& ent, const float* gent);
+void launch_rescal_apply(const RelArgs& P, const TabView& ent, const float* gent, float lr, float clip,
+                         hipStream_t st);
 // lambda * (mean_e ||e||^2 + mean_r ||R_r||_F^2) added to the step loss (RESCAL.py:190-198)
 void launch_reg_loss(const TabView& ent, const TabView& rel, float lam, float* part, StepCtl* ctl,
                      float* loss_out, float* loss_accum, uint32_t sig, int32_t* status, hipStream_t st);

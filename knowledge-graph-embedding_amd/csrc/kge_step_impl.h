@@ -39,6 +39,9 @@
 #ifndef KGE_STREAM_ROWS
 #define KGE_STREAM_ROWS 8   // sampled rows per stream batch at NC = 1 (tuning knob)
 #endif
+#ifndef KGE_UPD_COMPACT_WPE
+#define KGE_UPD_COMPACT_WPE 8   // compact update launch: amdgpu_waves_per_eu (tuning knob)
+#endif
 #ifndef KGE_COMPACT_LIST0
 #define KGE_COMPACT_LIST0 1 // compact launches: list position 0 lives only in the leader table (A-B knob)
 #endif
@@ -224,7 +227,7 @@ __device__ __forceinline__ float frag_elem_bcast(const Frag<VEC, NC>& f, int i) 
 
 // RESCAL context products of one positive (RESCAL.py:166-171), shared by its
 // waves: this wave takes rows [rb, re) of R (row i at Rm + i d) in batches
-// of 8 (every row's load issued before use) and accumulates
+// of 16 (every row's load issued before use) and accumulates
 //   u-like  up += x_i R_i            (u = R^T x: the wave's partial)
 //   v-like  vl[i] = R_i . y          (v = R y: one transposed 8-row reduction)
 // The callers sum the waves' partials of u in wave order (LDS).
@@ -232,10 +235,10 @@ template <int VEC, int NC>
 __device__ void rel_gemv_pair(const float* __restrict__ Rm, int d, int rb, int re, const Frag<VEC, NC>& x,
                               const Frag<VEC, NC>& y, Frag<VEC, NC>& up, float* vl) {
   using F = Frag<VEC, NC>;
-  constexpr int NB = 8, SH = 3;
+  constexpr int NB = 16, SH = 2;   // lane l holds row (l >> SH) of the batch after multi_reduce
   up.zero();
   for (int i0 = rb; i0 < re; i0 += NB) {
-    F Rr[NB];
+    F Rr[NB];   // rows past re repeat the last one (weight 0, result dropped)
 #pragma unroll
     for (int u = 0; u < NB; ++u) load_row(Rr[u], Rm + (int64_t)min(i0 + u, re - 1) * d, d);
     float part[NB];
@@ -446,7 +449,10 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
       static_for<ROWS>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
         M::template fwdk<kind_at<SIDE>(u)>(ctx, E[u], a[u], b[u]);
-        part[u] = (u < nrow && (!RAW || lane_in)) ? score_partial<SK, M::CPLX>(a[u], b[u], A.p) : 0.f;
+        float pu;
+        if constexpr (M::FAST_STREAM) pu = M::template fast_partial<SK>(a[u], b[u]);
+        else pu = score_partial<SK, M::CPLX>(a[u], b[u], A.p);
+        part[u] = (u < nrow && (!RAW || lane_in)) ? pu : 0.f;
       });
       const float Rl = multi_reduce<ROWS, SK == SK_PINF>(part);
       float tl = 1.f;
@@ -845,7 +851,10 @@ __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(UW)
 void update_kernel(StepArgs A) {
   using M = Model<VEC, NC, SK>;
   using F = Frag<VEC, NC>;
-  constexpr int U = KGE_UPDATE_U / NC > 1 ? KGE_UPDATE_U / NC : 2;   // entries in flight per wave
+  // entries in flight per wave; the compact instance (8 waves / SIMD: 64
+  // VGPRs) takes 4 -- 8 spilled 28 bytes per lane (C2-50M KU 170 -> 160 us)
+  constexpr int UU = UW >= 8 ? 4 : KGE_UPDATE_U;
+  constexpr int U = UU / NC > 1 ? UU / NC : 2;
   constexpr int RV = RelV<M::CPLX, VEC>::n;
   constexpr int CHMAX = 4;                            // in-register ordering up to 256 codes
   __shared__ uint32_t s_scr[kUpdWaves][CHMAX * KGE_WAVE];
@@ -1272,7 +1281,8 @@ static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_
   if (A.train) {
     if constexpr (NC == 1 && !Model<VEC, NC, SK>::WIDE) {
       if (A.compact) {
-        hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK, 8>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
+        hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK, KGE_UPD_COMPACT_WPE>), dim3(G.gridU), dim3(kUpdThreads), 0,
+                           st, A);
         return KGE_OK;
       }
     }

@@ -14,7 +14,7 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = ("score_kernel", "update_kernel", "constrain_rows_kernel", "apply_kernel")
+KERNELS = ("score_kernel", "update_kernel", "constrain_rows_kernel", "apply_kernel", "rank_count_kernel")
 
 
 def short(name):
