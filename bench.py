@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--force-exchange", action="store_true",
                     help="one GPU: run the multi-GPU step (c5: all-to-all exchange + row cache instead of the "
                          "one-rank shortcut; other workloads: the sharded step with its exchange) as a rehearsal")
+    ap.add_argument("--loopback", action="store_true",
+                    help="with --force-exchange: every id (own ones too) through the exchange blocks -- the "
+                         "remote path's kernels and copies on one GPU")
     return ap.parse_args()
 
 
@@ -181,8 +184,9 @@ def build_model(w, E, R, rank, dev):
         # the reference initialiser, drawn on the device (a host draw of 40 GB would dominate)
         g = torch.Generator(device=dev).manual_seed(12345)
         lim = 6.0 / np.sqrt(d)
-        m.model_weights = {"ent_emb": (torch.rand((E, d), generator=g, device=dev) * 2 - 1).mul_(lim),
-                           "rel_emb": (torch.rand((R, d), generator=g, device=dev) * 2 - 1).mul_(lim)}
+        # (in place: no second E x d temporary -- C5's table is a third of HBM)
+        m.model_weights = {"ent_emb": torch.rand((E, d), generator=g, device=dev).mul_(2).sub_(1).mul_(lim),
+                           "rel_emb": torch.rand((R, d), generator=g, device=dev).mul_(2).sub_(1).mul_(lim)}
     else:
         m._init_embeddings(seed=12345)          # identical init on every rank
         m._to_device()
@@ -544,7 +548,7 @@ def main():
     if sharded:
         from KGE.sharded import ShardedStep
         step = ShardedStep(model, mode="sparse" if w.get("sharded") else "auto",
-                           local_fast=not args.force_exchange)
+                           local_fast=not args.force_exchange, loopback=args.loopback, batch_hint=B)
         if E > 10_000_000:
             step.release_entity_tables()   # the shard is the only copy the step needs
     else:
@@ -672,7 +676,7 @@ def main():
     }
     if sharded:
         out["config"]["exchange"] = "local (one rank: fused step on the shard)" if step.direct is not None \
-            else step.mode
+            else step.mode + (" (loopback: every id through the blocks)" if args.loopback else "")
     _RESULT_OUT.write(json.dumps(out) + "\n")
     _RESULT_OUT.flush()
     if sharded:

@@ -117,14 +117,31 @@ enum {
   KGE_FLAG_DEBUG_UNFUSED_CONSTRAINT = 4, /* test hook: run the full-table renormalisation
                                        as its own kernel even on the SGD path */
   KGE_FLAG_GRAD_ROWS_TOUCHED = 8,    /* KGE_OPT_GRAD: the caller needs only the entity
-                                       gradient rows the batch touches (a row cache of
-                                       exactly the batch's ids): no zero-fill of grad_out[0/3] */
-  KGE_FLAG_GRAD_RENORM = 16          /* KGE_OPT_GRAD, TransE / DistMult with constraint:
+                                       gradient rows the batch touches: grad_out[0/3] are
+                                       written at those rows only (no zero-fill), so they may
+                                       address just the range the batch's ids fall in */
+  KGE_FLAG_GRAD_RENORM = 16,         /* KGE_OPT_GRAD, TransE / DistMult with constraint:
                                        the renormalisation assign runs inside the step as on
                                        the SGD path (rows scored normalised in registers) and
                                        the step writes every entity row back normalised; the
                                        caller applies its update to those rows (no full-table
                                        pass of its own) */
+  /* Split step (the multi-GPU sparse exchange, KGE/sharded.py; TransE /
+   * DistMult / RotatE with KGE_OPT_SGD): the same descriptor is passed twice
+   * with the same workspace --
+   *   PHASE_SCORE   the draws and the score pass: loss_out and norm2_out get
+   *                 THIS call's (local) loss and per-variable slice norm^2; no
+   *                 update;
+   *   PHASE_UPDATE  the update pass alone, its clip scales from norm2_out (the
+   *                 caller may have all-reduced them in between); entity rows
+   *                 >= remote_rows_from receive their summed raw gradient IN
+   *                 PLACE of the row (rows fetched from another rank, sent back
+   *                 to their owner), the others the clipped SGD update;
+   *                 relation rows' summed raw gradients go to grad_out[1]
+   *                 (zero-filled by the call) for the caller to reduce and apply;
+   *                 nothing at all when abort_flag is set and *abort_flag != 0. */
+  KGE_FLAG_PHASE_SCORE = 32,
+  KGE_FLAG_PHASE_UPDATE = 64
 };
 
 typedef struct kge_table {
@@ -238,6 +255,9 @@ typedef struct kge_step_desc {
   int64_t global_entities;
   int32_t shard_count;
   int32_t _pad3;
+  /* KGE_FLAG_PHASE_UPDATE (see the flags): */
+  int64_t remote_rows_from;   /* entity rows >= this get their raw gradient in place (0: none) */
+  const float* abort_flag;    /* device [1]; nonzero: the update pass does nothing (nullable) */
 } kge_step_desc;
 
 /*
@@ -264,6 +284,8 @@ typedef struct kge_apply_desc {
   float beta_1, beta_2, epsilon;
   int32_t _pad2;
   int64_t iteration;          /* ADAM step t >= 1 (optimizer.iterations + 1)   */
+  const float* abort_flag;    /* device [1]; nonzero: nothing is applied (nullable; the
+                                 multi-GPU step's all-reduced exchange error flag) */
 } kge_apply_desc;
 
 /*
@@ -366,6 +388,80 @@ typedef struct kge_stream_desc {
 } kge_stream_desc;
 
 kge_status kge_stream_batch(const kge_stream_desc* d, void* stream);
+
+/*
+ * Multi-GPU sparse row exchange (KGE/sharded.py; the reference has no
+ * counterpart, BaseModel.py:19-21 is single-device). Entity row e lives on
+ * rank e mod G at local row e div G. A rank's step needs the rows of its
+ * batch's ids; those another rank owns travel in FIXED-CAPACITY blocks of cap
+ * rows per owner, so every collective has static sizes and nothing waits on
+ * the host. A rank's extended entity table is [local_rows owned rows | G blocks
+ * of cap fetched rows] (block `rank` holds own rows only with loopback).
+ *
+ * kge_exchange_plan: the step's id occurrences (positives' h and t, the
+ * negatives) -> the same arrays in extended-table rows (pos_out, neg_out), and
+ * per owner the distinct ids requested from it (req_ids [world, cap],
+ * req_cnt [world]). Own ids map to their shard row directly (loopback: every
+ * id through its owner's block -- a one-GPU rehearsal of the remote path). A
+ * block past cap, or an id out of range, sets *err_flag: the caller's step is
+ * then void (its update pass and every owner apply check the all-reduced flag).
+ */
+typedef struct kge_exchange_desc {
+  int32_t abi_version;        /* KGE_ABI_VERSION                                */
+  int32_t idx_dtype;          /* KGE_IDX_* of pos / neg / req_ids / outputs      */
+  const void* pos;            /* [batch, 3] global ids                           */
+  const void* neg;            /* [n_neg] global negative ids                     */
+  int64_t batch, n_neg;
+  int64_t n_entities;         /* global E (range check), < 2^32 - 1              */
+  int32_t world, rank;
+  int32_t loopback;           /* 1: own ids fetched through block `rank` as well */
+  int32_t _pad;
+  int64_t local_rows;         /* owned rows at the head of the extended table    */
+  int64_t cap;                /* rows per owner block                            */
+  unsigned long long* htab;   /* [hslots], zero-filled by the caller before each call */
+  int64_t hslots;             /* power of two >= 2 (2 batch + n_neg)             */
+  void* pos_out;              /* [batch, 3]: h, t remapped, r copied              */
+  void* neg_out;              /* [n_neg] remapped                                */
+  void* req_ids;              /* [world, cap] out                                */
+  int32_t* req_cnt;           /* [world] out, zero-filled by the caller          */
+  float* err_flag;            /* device [1]: set to 1 on an overflow / bad id (nullable) */
+  int32_t* status;            /* KGE_ERANGE on an id out of range (nullable)     */
+} kge_exchange_desc;
+
+kge_status kge_exchange_plan(const kge_exchange_desc* d, void* stream);
+
+/* Owner side of the exchange, over requested ids [world, cap] (cnt [world]):
+ *  KGE_XROWS_GATHER  rows[s][q] = shard row (ids[s][q] div world), every block
+ *                    (source < 0) or block `source`;
+ *  KGE_XROWS_SGD     shard row += -lr * clip / max(sqrt(*norm2), clip) * rows[s][q]
+ *                    for block s = source (keras SGD after clip_by_norm,
+ *                    BaseModel.py:327-328); one call per source, in rank order,
+ *                    so a row several ranks touched gets their sums in that order;
+ *  KGE_XROWS_ACCUM   acc row += rows[s][q] for block `source` (Adam: the dense
+ *                    gradient of the shard, kge_apply follows).
+ * SGD / ACCUM do nothing when abort_flag is set and *abort_flag != 0. */
+enum { KGE_XROWS_GATHER = 0, KGE_XROWS_SGD = 1, KGE_XROWS_ACCUM = 2 };
+
+typedef struct kge_exchange_rows_desc {
+  int32_t mode;               /* KGE_XROWS_*                                     */
+  int32_t idx_dtype;          /* of ids                                          */
+  kge_table shard;            /* owned rows (a view: one table's columns, ld = row stride) */
+  const void* ids;            /* [world, cap]                                    */
+  const int32_t* cnt;         /* [world]                                         */
+  int32_t world, rank;
+  int32_t source;             /* block (GATHER: -1 = every block)                */
+  int32_t _pad;
+  int64_t cap;
+  float* rows;                /* [world, cap] rows, stride rows_ld (GATHER out, SGD / ACCUM in) */
+  int64_t rows_ld;
+  float* acc;                 /* ACCUM: [shard.rows, shard.cols], stride shard.cols */
+  const float* norm2;         /* SGD: the variable's global slice norm^2         */
+  float lr, clip_norm;
+  const float* abort_flag;    /* nullable                                        */
+  int32_t* status;            /* KGE_ERANGE on an id this rank does not own (nullable) */
+} kge_exchange_rows_desc;
+
+kge_status kge_exchange_rows(const kge_exchange_rows_desc* d, void* stream);
 
 /* ABI version compiled into the library. */
 int32_t kge_abi_version(void);

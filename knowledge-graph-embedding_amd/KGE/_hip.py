@@ -23,6 +23,8 @@ OPT_NONE, OPT_SGD, OPT_GRAD, OPT_ADAM = range(4)
 FLAG_NO_TABLE_CONSTRAINT = 1
 FLAG_GRAD_ROWS_TOUCHED = 8
 FLAG_GRAD_RENORM = 16
+FLAG_PHASE_SCORE = 32
+FLAG_PHASE_UPDATE = 64
 RANK_TRANS, RANK_ROT, RANK_MUL, RANK_DOT = range(4)
 RPROJ_NONE, RPROJ_HYPER, RPROJ_RANK1 = range(3)
 
@@ -72,6 +74,7 @@ class kge_step_desc(ctypes.Structure):
         ("grad_out", ctypes.c_void_p * 4),
         ("shard_rows", ctypes.c_int64), ("global_entities", ctypes.c_int64),
         ("shard_count", ctypes.c_int32), ("_pad3", ctypes.c_int32),
+        ("remote_rows_from", ctypes.c_int64), ("abort_flag", ctypes.c_void_p),
     ]
 
 
@@ -80,7 +83,7 @@ class kge_apply_desc(ctypes.Structure):
                 ("grad", ctypes.c_void_p), ("norm2", ctypes.c_void_p), ("lr", ctypes.c_float),
                 ("clip_norm", ctypes.c_float), ("m", ctypes.c_void_p), ("v", ctypes.c_void_p),
                 ("beta_1", ctypes.c_float), ("beta_2", ctypes.c_float), ("epsilon", ctypes.c_float),
-                ("_pad2", ctypes.c_int32), ("iteration", ctypes.c_int64)]
+                ("_pad2", ctypes.c_int32), ("iteration", ctypes.c_int64), ("abort_flag", ctypes.c_void_p)]
 
 
 class kge_rank_desc(ctypes.Structure):
@@ -100,6 +103,28 @@ class kge_apply_rows_desc(ctypes.Structure):
                 ("clip_norm", ctypes.c_float)]
 
 
+class kge_exchange_desc(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("idx_dtype", ctypes.c_int32), ("pos", ctypes.c_void_p),
+                ("neg", ctypes.c_void_p), ("batch", ctypes.c_int64), ("n_neg", ctypes.c_int64),
+                ("n_entities", ctypes.c_int64), ("world", ctypes.c_int32), ("rank", ctypes.c_int32),
+                ("loopback", ctypes.c_int32), ("_pad", ctypes.c_int32), ("local_rows", ctypes.c_int64),
+                ("cap", ctypes.c_int64), ("htab", ctypes.c_void_p), ("hslots", ctypes.c_int64),
+                ("pos_out", ctypes.c_void_p), ("neg_out", ctypes.c_void_p), ("req_ids", ctypes.c_void_p),
+                ("req_cnt", ctypes.c_void_p), ("err_flag", ctypes.c_void_p), ("status", ctypes.c_void_p)]
+
+
+XROWS_GATHER, XROWS_SGD, XROWS_ACCUM = range(3)
+
+
+class kge_exchange_rows_desc(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("idx_dtype", ctypes.c_int32), ("shard", kge_table),
+                ("ids", ctypes.c_void_p), ("cnt", ctypes.c_void_p), ("world", ctypes.c_int32),
+                ("rank", ctypes.c_int32), ("source", ctypes.c_int32), ("_pad", ctypes.c_int32),
+                ("cap", ctypes.c_int64), ("rows", ctypes.c_void_p), ("rows_ld", ctypes.c_int64),
+                ("acc", ctypes.c_void_p), ("norm2", ctypes.c_void_p), ("lr", ctypes.c_float),
+                ("clip_norm", ctypes.c_float), ("abort_flag", ctypes.c_void_p), ("status", ctypes.c_void_p)]
+
+
 class kge_stream_desc(ctypes.Structure):
     _fields_ = [("abi_version", ctypes.c_int32), ("idx_dtype", ctypes.c_int32), ("triples", ctypes.c_void_p),
                 ("n_rows", ctypes.c_int64), ("start", ctypes.c_int64), ("batch", ctypes.c_int64),
@@ -109,7 +134,8 @@ class kge_stream_desc(ctypes.Structure):
 
 EXPORTS = ("kge_abi_version", "kge_last_error", "kge_step_workspace_bytes", "kge_step_plan_signature", "kge_step",
            "kge_sample",
-           "kge_apply", "kge_constrain_rows", "kge_rank", "kge_apply_rows", "kge_stream_batch")
+           "kge_apply", "kge_constrain_rows", "kge_rank", "kge_apply_rows", "kge_stream_batch", "kge_exchange_plan",
+           "kge_exchange_rows")
 
 _lock = threading.Lock()
 _lib = None
@@ -144,6 +170,10 @@ def load(path=LIB_PATH):
         L.kge_rank.argtypes = [ctypes.POINTER(kge_rank_desc), ctypes.c_void_p]
         L.kge_stream_batch.restype = ctypes.c_int
         L.kge_stream_batch.argtypes = [ctypes.POINTER(kge_stream_desc), ctypes.c_void_p]
+        L.kge_exchange_plan.restype = ctypes.c_int
+        L.kge_exchange_plan.argtypes = [ctypes.POINTER(kge_exchange_desc), ctypes.c_void_p]
+        L.kge_exchange_rows.restype = ctypes.c_int
+        L.kge_exchange_rows.argtypes = [ctypes.POINTER(kge_exchange_rows_desc), ctypes.c_void_p]
         L.kge_constrain_rows.restype = ctypes.c_int
         L.kge_constrain_rows.argtypes = [kge_table, ctypes.c_int32, ctypes.c_float, ctypes.c_void_p]
         if L.kge_abi_version() != ABI_VERSION:

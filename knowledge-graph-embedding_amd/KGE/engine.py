@@ -162,6 +162,15 @@ class FusedStep:
         self.plane_fn = None          # optional: planes -> first plane (multi-GPU offsets)
         self.shard = None             # optional (G, shard_rows, global E): the tables are gathered shards
         self.names = fused_names(model) if tables is not None else None   # weight keys by role (Adam slots)
+        # split step (KGE/sharded.py, KGE_FLAG_PHASE_*): rows >= remote_from get
+        # their raw gradient in place; relation gradients into rel_grad_out;
+        # the update pass skipped when *abort != 0
+        self.remote_from = None
+        self.rel_grad_out = None
+        self.abort = None
+        self.grad_row_offset = 0      # grad mode: entity gradient buffers start at this table row
+        self._descs = {}              # call key -> (descriptor, plan signature)
+        self._ws_sig = None
 
     def _tables(self):
         return self.tables if self.tables is not None else self.model._fused_tables()
@@ -243,7 +252,15 @@ class FusedStep:
             g = self.grad_buffers()
             slot = {"ent": 0, "rel": 1, "rel_aux": 2, "ent_aux": 3}
             for role, buf in zip(self.grad_roles(), g):
-                d.grad_out[slot[role]] = buf.data_ptr()
+                off = self.grad_row_offset * buf.shape[1] * 4 if role in ("ent", "ent_aux") else 0
+                # (KGE_FLAG_GRAD_ROWS_TOUCHED: the step writes rows >= the offset only)
+                d.grad_out[slot[role]] = buf.data_ptr() - off
+        elif self.rel_grad_out is not None:
+            d.grad_out[1] = self.rel_grad_out.data_ptr()
+        if self.remote_from is not None:
+            d.remote_rows_from = int(self.remote_from)
+        if self.abort is not None:
+            d.abort_flag = self.abort.data_ptr()
         d.loss_out = self.loss_out.data_ptr()
         d.loss_accum = self.loss_accum.data_ptr()
         d.norm2_out = self.norm2.data_ptr()
@@ -274,10 +291,12 @@ class FusedStep:
                      for r in ("ent", "rel", "ent_aux", "rel_aux")),
                tuple((g.data_ptr(), tuple(g.shape)) for g in self.grads) if self.grads is not None else None,
                id(m.ns_strategy), m.negative_ratio, m.corrupt_side, self.batch_scale, self.cw_scale, self.flags,
-               float(getattr(m, "constraint_weight", 0.0)))
-        cached = getattr(self, "_cache", None)
-        if cached is not None and cached[0] == key:
-            d = cached[1]
+               float(getattr(m, "constraint_weight", 0.0)), self.remote_from, self.grad_row_offset,
+               self.rel_grad_out.data_ptr() if self.rel_grad_out is not None else None,
+               self.abort.data_ptr() if self.abort is not None else None)
+        hit = self._descs.get(key)
+        if hit is not None:
+            d, sig = hit
             d.pos = batch.data_ptr()
             if neg_ids is not None:
                 d.neg_ids = neg_ids.data_ptr()
@@ -287,6 +306,9 @@ class FusedStep:
                 d.pos_score_out = pos_score.data_ptr()
             if neg_score is not None:
                 d.neg_score_out = neg_score.data_ptr()
+            if sig != self._ws_sig:   # another cached plan ran in between
+                self.workspace.zero_()
+                self._ws_sig = sig
         else:
             d = self.describe(batch, is_train, optimizer, neg_ids, pos_score, neg_score)
             need = int(self.lib.kge_step_workspace_bytes(d))
@@ -297,14 +319,17 @@ class FusedStep:
                 # zero-filled once: the step's tickets / destination counters
                 # live in the workspace and reset themselves between calls
                 self.workspace = torch.zeros(need, dtype=torch.uint8, device=self.device)
-            elif sig != getattr(self, "_ws_sig", None):
+                self._descs.clear()   # (they point at the old buffer)
+            elif sig != self._ws_sig:
                 # a different plan lays the workspace out differently (the
                 # library would refuse the stamped buffer): zeros again
                 self.workspace.zero_()
             self._ws_sig = sig
             d.workspace = self.workspace.data_ptr()
             d.workspace_bytes = self.workspace.numel()
-            self._cache = (key, d)
+            if len(self._descs) >= 8:
+                self._descs.clear()
+            self._descs[key] = (d, sig)   # (the split step alternates two descriptors)
         d.prof_events = ctypes.cast(prof_events, ctypes.c_void_p) if prof_events is not None else None
         d.loss_accum = (accum if accum is not None else self.loss_accum).data_ptr()
         _hip.check(self.lib.kge_step(d, _hip.stream_handle(self.device)), "kge_step")
@@ -312,9 +337,12 @@ class FusedStep:
             self.apply_adam(optimizer)
         return self.loss_out
 
-    def apply(self, var, grad, norm2_ptr, optimizer, name=None):
-        """``kge_apply`` of one variable (SGD or keras Adam) with global norm^2 at ``norm2_ptr``."""
+    def apply(self, var, grad, norm2_ptr, optimizer, name=None, abort=None):
+        """``kge_apply`` of one variable (SGD or keras Adam) with global norm^2
+        at ``norm2_ptr``; nothing applied when ``abort`` (device float [1]) is nonzero."""
         a = _hip.kge_apply_desc()
+        if abort is not None:
+            a.abort_flag = abort.data_ptr()
         a.var = _hip.table(var)
         a.grad = grad.data_ptr()
         a.norm2 = norm2_ptr

@@ -202,7 +202,7 @@ class KGEModel:
             if self._fused is None:
                 if world > 1:
                     from ...sharded import ShardedStep
-                    self._fused = ShardedStep(self)
+                    self._fused = ShardedStep(self, batch_hint=batch_data.shape[0] // world)
                 else:
                     self._fused = engine.FusedStep(self)
             if world > 1:

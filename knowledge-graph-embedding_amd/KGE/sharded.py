@@ -58,6 +58,7 @@ from . import optimizers as _opt
 from .constraint import clip_constraint, normalized_embeddings
 
 _RENORM = (_hip.MODEL_TRANSE, _hip.MODEL_DISTMULT)
+_SPLIT = (_hip.MODEL_TRANSE, _hip.MODEL_DISTMULT, _hip.MODEL_ROTATE)   # the split (two-pass) SGD step
 _CLIP = (_hip.MODEL_TRANSR, _hip.MODEL_TRANSD)
 DENSE_TABLE_BYTES = 1 << 30   # "auto": replicated tables + one all-reduce below this entity-table size
 
@@ -79,7 +80,8 @@ class Exchange:
             dist.all_gather(list(full.chunk(self.world)), shard, group=self.group)
 
     def all_reduce(self, t):
-        dist.all_reduce(t, group=self.group)
+        if self.world > 1:   # (one rank: the sum is the tensor itself)
+            dist.all_reduce(t, group=self.group)
 
     def all_to_all(self, out, inp, out_splits=None, in_splits=None):
         dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
@@ -88,7 +90,15 @@ class Exchange:
 class ShardedStep:
     """Drop-in for ``FusedStep`` across G ranks (see module docstring)."""
 
-    def __init__(self, model, exchange=None, mode="auto", local_fast=True):
+    def __init__(self, model, exchange=None, mode="auto", local_fast=True, loopback=False, capacity_slack=1.1,
+                 capacity_floor=1024, batch_hint=None):
+        """``loopback`` (sparse mode): own ids too go through the exchange blocks
+        (a one-GPU rehearsal of the remote path). Each owner block holds
+        ceil(capacity_slack * occurrences / G) + capacity_floor rows; a step
+        whose ids overflow a block is skipped on every rank and reported by
+        check_status(). ``batch_hint`` (positives per rank per step) sizes the
+        exchange blocks up front, so the owned rows are allocated once, at the
+        head of the extended table (no second copy of a shard that fills HBM)."""
         self.model = model
         self.ex = exchange or Exchange()
         G, g = self.ex.world, self.ex.rank
@@ -124,9 +134,18 @@ class ShardedStep:
             raise NotImplementedError("sharded step: a full-table regulariser (RESCAL, TransH with constraint) "
                                       "has a dense gradient of every row -- use the dense exchange")
         self.mode = mode
+        self.loopback = bool(loopback)
+        self.slack = float(capacity_slack)
+        self.cap_floor = int(capacity_floor)
+        self._ext = None
+        self._needs_loop = False
         if mode == "sparse":
-            # owned rows [ent | ent_aux], padded to Es rows
-            self.shard = torch.zeros(self.Es, C, dtype=torch.float32, device=dev)
+            # owned rows [ent | ent_aux], padded to Es rows (on a GPU: the head of
+            # the extended table, the fetched blocks follow -- _ext_for)
+            if batch_hint and dev.type == "cuda":
+                self._ext_for(self._occurrences(int(batch_hint)), torch.int64, fill=False)
+            else:
+                self.shard = torch.zeros(self.Es, C, dtype=torch.float32, device=dev)
             self.shard[:self.valid, :self.ce] = ent.reshape(E, -1)[g::G]
             if self.ca:
                 self.shard[:self.valid, self.ce:] = t["ent_aux"].reshape(E, -1)[g::G]
@@ -176,7 +195,7 @@ class ShardedStep:
         # one rank: every row is local, so the fused single-device step runs on
         # the shard itself (in-kernel SGD, compact update launch) -- no cache
         self.direct = None
-        if self.fused is not None and G == 1 and mode == "sparse" and local_fast:
+        if self.fused is not None and G == 1 and mode == "sparse" and local_fast and not self.loopback:
             td = dict(t)
             td["ent"] = self.shard[:, :self.ce].view(self.ent_shape)
             if self.ca:
@@ -420,19 +439,19 @@ class ShardedStep:
     def _shard_name(self, k):
         return self.names["ent" if k == 0 else "ent_aux"] + "#shard"
 
-    def _apply_dense(self, var, grad, v, optimizer, name):
+    def _apply_dense(self, var, grad, v, optimizer, name, abort=None):
         if var.shape[0] == 0:
             return
         if self.fused is not None:
-            self.fused.apply(var, grad, self.norm2.data_ptr() + 4 * v, optimizer, name)
+            self.fused.apply(var, grad, self.norm2.data_ptr() + 4 * v, optimizer, name, abort=abort)
         else:
             _host_apply(var, grad, self.norm2[v], optimizer, name)
 
-    def _apply_rel(self, optimizer):
+    def _apply_rel(self, optimizer, abort=None):
         slot = {"rel": 1, "rel_aux": 2}
         for r in self.rel_roles:
             w = self.tables[r]
-            self._apply_dense(w.view(w.shape[0], -1), self.grel[r], slot[r], optimizer, self.names[r])
+            self._apply_dense(w.view(w.shape[0], -1), self.grel[r], slot[r], optimizer, self.names[r], abort=abort)
 
     # ------------------------------------------------------------ step
     def __call__(self, batch, is_train, optimizer, neg_ids=None, prof_events=None):
@@ -462,6 +481,8 @@ class ShardedStep:
             return self.loss
         if neg_ids is None:
             neg_ids = self._draw(batch)
+        if self.fused is not None:
+            return self._sparse_device(batch, is_train, optimizer, neg_ids.to(batch.dtype).contiguous(), prof_events)
         Bn = int(batch.shape[0])
         ids = torch.cat([batch[:, 0], batch[:, 2], neg_ids.to(batch.dtype)]).to(torch.int64)
         self._bmax = max(getattr(self, "_bmax", 0), Bn)
@@ -477,6 +498,215 @@ class ShardedStep:
             self._apply_sparse(optimizer, gbufs, *plan)
             self._apply_rel(optimizer)
         return self.loss
+
+    # ------------------------------------------------------------ device sparse exchange
+    def _occurrences(self, B):
+        """Entity id occurrences of a B-positive step (h, t, negatives)."""
+        m = self.model
+        K = int(m.negative_ratio)
+        return B * (2 + (2 * (K // 2) if m.corrupt_side == "h+t" else K))
+
+    def _ext_for(self, n_occ, idx_dtype, fill=True):
+        """Fixed-capacity exchange buffers for steps of up to n_occ id
+        occurrences (sized once for the largest step seen, so the step's plan
+        never changes): the extended table [Es owned rows | G blocks of cap
+        fetched rows] whose head IS the shard, the request / receive id
+        blocks, send rows, the hash table."""
+        G = self.G
+        old = self._ext
+        if old is not None and old["n_occ"] >= n_occ:
+            if old["dtype"] != idx_dtype:   # same blocks, id arrays of the other width
+                for k in ("req_ids", "recv_ids"):
+                    if k in old:
+                        old[k] = torch.zeros(old[k].shape[0], dtype=idx_dtype, device=self.device)
+                if G == 1:
+                    old["recv_ids"] = old["req_ids"]
+                old["dtype"] = idx_dtype
+            return old
+        dev, C = self.device, self.C
+        remote = G > 1 or self.loopback or self._needs_loop
+        cap = max(1, int(math.ceil(self.slack * n_occ / G)) + self.cap_floor) if remote else 1
+        rows = self.Es + G * cap
+        if dev.type == "cuda" and rows * C * 4 > (1 << 32):
+            torch.cuda.empty_cache()   # a shard that fills HBM: hand cached blocks back first
+        ext = torch.zeros(rows, C, dtype=torch.float32, device=dev)
+        if fill:
+            ext[:self.Es] = self.shard
+        self.shard = ext[:self.Es]       # the owned rows live at the head of the extended table
+        self._ext = None
+        del old
+        self.direct = None
+        hs = 1
+        while hs < 2 * n_occ:
+            hs <<= 1
+        b = {"n_occ": n_occ, "dtype": idx_dtype, "cap": cap, "ext": ext, "hslots": hs,
+             "htab": torch.zeros(hs, dtype=torch.int64, device=dev),
+             "req_cnt": torch.zeros(G, dtype=torch.int32, device=dev),
+             "req_ids": torch.zeros(G * cap, dtype=idx_dtype, device=dev),
+             "err": torch.zeros(1, dtype=torch.float32, device=dev)}
+        if G > 1:
+            b["recv_cnt"] = torch.zeros(G, dtype=torch.int32, device=dev)
+            b["recv_ids"] = torch.zeros(G * cap, dtype=idx_dtype, device=dev)
+            b["send"] = torch.zeros(G * cap, C, dtype=torch.float32, device=dev)
+        else:   # one rank: the owner side reads the request blocks, fetched rows land in place
+            b["recv_cnt"], b["recv_ids"] = b["req_cnt"], b["req_ids"]
+        self._ext = b
+        return b
+
+    def _xrows(self, b, mode, rows, rows_ld, view, source=-1, norm2_ptr=None, lr=0.0, acc=None):
+        """kge_exchange_rows on this rank's owned rows ``view`` (a column view of the shard)."""
+        d = _hip.kge_exchange_rows_desc()
+        d.mode = mode
+        d.idx_dtype = _hip.IDX_I64 if b["dtype"] == torch.int64 else _hip.IDX_I32
+        d.shard = _hip.table(view)
+        d.ids = b["recv_ids"].data_ptr()
+        d.cnt = b["recv_cnt"].data_ptr()
+        d.world, d.rank, d.source = self.G, self.g, source
+        d.cap = b["cap"]
+        d.rows = rows.data_ptr()
+        d.rows_ld = rows_ld
+        d.acc = acc.data_ptr() if acc is not None else None
+        d.norm2 = norm2_ptr
+        d.lr = lr
+        d.clip_norm = 5.0
+        d.abort_flag = self.red[-1:].data_ptr()   # the all-reduced exchange error flag
+        d.status = self.status.data_ptr()
+        _hip.check(self.lib.kge_exchange_rows(ctypes.byref(d), _hip.stream_handle(self.device)), "kge_exchange_rows")
+
+    def _split_fused(self):
+        """The element-wise models' SGD step in two passes (KGE_FLAG_PHASE_*)."""
+        if getattr(self, "_sf", None) is None:
+            f = engine.FusedStep(self.model, tables=dict(self.tables))
+            f.norm2 = self.norm2
+            f.loss_out = self.loss
+            f.status = self.status
+            f.batch_scale = float(self.G)
+            f.rel_grad_out = self.grel["rel"]
+            self._sf = f
+        return self._sf
+
+    def _sparse_device(self, batch, is_train, optimizer, neg, prof_events):
+        """One sparse step with no host synchronisation (KGE/sharded.py module
+        docstring): kge_exchange_plan on the device, collectives of static
+        sizes, the step on the extended table, gradients back, owner applies
+        in rank order.
+
+        Element-wise models (TransE / DistMult / RotatE) with SGD run the split
+        step: score pass -> all-reduce [norm^2 | loss | error flag] -> update
+        pass (owned rows updated in place with the global clip scale, fetched
+        rows replaced by their raw gradients, relation gradients out) ->
+        all-reduce of the relation gradients -> the fetched rows' gradients
+        back to their owners. The other models, Adam and validation steps run
+        one gradient-mode step with every id through the blocks (loopback):
+        gradient rows back, owners apply (SGD) or accumulate them (Adam)."""
+        G, g = self.G, self.g
+        Bn = int(batch.shape[0])
+        n_neg = int(neg.shape[0])
+        split = self.mid in _SPLIT and is_train and isinstance(optimizer, _opt.SGD)
+        loop = self.loopback or not split
+        if loop and not self.loopback and G == 1 and (self._ext is None or self._ext["cap"] == 1):
+            self._needs_loop = True    # a one-rank gradient-mode step needs the blocks
+            if self._ext is not None:
+                self._ext["n_occ"] = -1   # re-plan the blocks
+        b = self._ext_for(2 * Bn + n_neg, batch.dtype)
+        cap, ext, C = b["cap"], b["ext"], self.C
+        st = _hip.stream_handle(self.device)
+        # 1. plan: the triples / negatives in extended-table rows, request blocks
+        b["htab"].zero_()
+        b["req_cnt"].zero_()
+        b["err"].zero_()
+        lpos = torch.empty_like(batch)
+        lneg = torch.empty_like(neg)
+        x = _hip.kge_exchange_desc()
+        x.abi_version = _hip.ABI_VERSION
+        x.idx_dtype = _hip.IDX_I64 if batch.dtype == torch.int64 else _hip.IDX_I32
+        x.pos, x.neg = batch.data_ptr(), neg.data_ptr()
+        x.batch, x.n_neg = Bn, n_neg
+        x.n_entities = self.E
+        x.world, x.rank, x.loopback = G, g, int(loop)
+        x.local_rows = self.Es
+        x.cap = cap
+        x.htab, x.hslots = b["htab"].data_ptr(), b["hslots"]
+        x.pos_out, x.neg_out = lpos.data_ptr(), lneg.data_ptr()
+        x.req_ids, x.req_cnt = b["req_ids"].data_ptr(), b["req_cnt"].data_ptr()
+        x.err_flag = b["err"].data_ptr()
+        x.status = self.status.data_ptr()
+        _hip.check(self.lib.kge_exchange_plan(ctypes.byref(x), st), "kge_exchange_plan")
+        # 2. requests to the owners, owners gather, rows back
+        blocks = ext[self.Es:]
+        if G > 1:
+            self.ex.all_to_all(b["recv_cnt"], b["req_cnt"])
+            self.ex.all_to_all(b["recv_ids"], b["req_ids"])
+            self._xrows(b, _hip.XROWS_GATHER, b["send"], C, self.shard)
+            self.ex.all_to_all(blocks, b["send"])
+        elif loop:
+            self._xrows(b, _hip.XROWS_GATHER, blocks, C, self.shard)
+        lt = self._local_tables(ext)
+        small = self.red[-8:]     # [norm^2 x4 | loss | - | - | exchange error flag]
+        if split:
+            # 3a. score pass, global norms / loss / error, update pass
+            f = self._split_fused()
+            f.tables = lt
+            f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_PHASE_SCORE
+            f(lpos, True, optimizer, neg_ids=lneg, prof_events=prof_events)
+            small[-1:].copy_(b["err"])
+            if G > 1:
+                self.ex.all_reduce(small)
+            f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_PHASE_UPDATE
+            f.remote_from = self.Es
+            f.abort = small[-1:]
+            f(lpos, True, optimizer, neg_ids=lneg)
+            if G > 1:
+                self.ex.all_reduce(self.red[:-8])   # relation gradients
+            grad_blocks = [blocks]
+        else:
+            # 3b. one gradient-mode step: every entity gradient row in the blocks
+            f = self.fused
+            f.tables = lt
+            gb = self._gblocks(b)
+            f.grads = [gb[0], self.grel["rel"]] + ([self.grel["rel_aux"]] if "rel_aux" in self.grel else []) + \
+                ([gb[1]] if self.ca else [])
+            f.grad_row_offset = self.Es   # the step addresses rows >= Es only (all ids through the blocks)
+            f(lpos, is_train, optimizer if is_train else None, neg_ids=lneg, prof_events=prof_events)
+            small[-1:].copy_(b["err"])
+            if G > 1:
+                self.ex.all_reduce(self.red)
+            grad_blocks = gb
+        if not is_train:
+            return self.loss
+        # 4. the fetched rows' gradients back to their owners; owners apply
+        # them source by source in rank order (SGD) or add them up (Adam: a
+        # dense keras Adam of the shard)
+        if G > 1 or loop:
+            adam = isinstance(optimizer, _opt.Adam)
+            for k, gk in enumerate(grad_blocks):
+                if G > 1:
+                    r = b["send"] if gk.shape[1] == C else torch.empty_like(gk)
+                    self.ex.all_to_all(r, gk)
+                    gk = r
+                lo = 0 if k == 0 else self.ce
+                cols = self._ecols()[k]
+                view = self.shard[:, lo:lo + cols]
+                if adam:
+                    acc = torch.zeros(self.Es, cols, dtype=torch.float32, device=self.device)
+                    for s in range(G):
+                        self._xrows(b, _hip.XROWS_ACCUM, gk, gk.stride(0), view, source=s, acc=acc)
+                    self._apply_dense(view[:self.valid], acc[:self.valid], self._slot(k), optimizer,
+                                      self._shard_name(k), abort=small[-1:])
+                else:
+                    for s in range(G):
+                        self._xrows(b, _hip.XROWS_SGD, gk, gk.stride(0), view, source=s,
+                                    norm2_ptr=self.norm2.data_ptr() + 4 * self._slot(k),
+                                    lr=optimizer.learning_rate)
+        self._apply_rel(optimizer, abort=small[-1:])
+        return self.loss
+
+    def _gblocks(self, b):
+        """Gradient rows of the fetched blocks [G cap, cols], per entity table."""
+        if "gblocks" not in b:
+            b["gblocks"] = [torch.zeros(self.G * b["cap"], c, dtype=torch.float32, device=self.device)
+                            for c in self._ecols()]
+        return b["gblocks"]
 
     # ------------------------------------------------------------ state
     def release_entity_tables(self):
@@ -550,6 +780,9 @@ class ShardedStep:
             self.direct.check_status()
         if self.fused is not None:
             _hip.check_device_status(self.status, "kge_step")
+        if self._ext is not None and float(self.red[-1]) != 0.0:
+            raise RuntimeError("sparse exchange: the step's ids overflowed an owner block (capacity %d rows); "
+                               "the step was skipped on every rank -- raise capacity_slack" % self._ext["cap"])
 
 
 def _host_apply(var, grad, norm2, optimizer, name):

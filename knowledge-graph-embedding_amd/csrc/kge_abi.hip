@@ -294,7 +294,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   // kernel, which writes the normalised row plus this step's SGD delta
   A.fuse_norm = fuse_norm_plan;
   A.compact = compact;
-  A.zero_untouched = A.grad_mode && !compact && !rescal && !transr && !proj;
+  A.zero_untouched = A.grad_mode && !compact && !rescal && !transr && !proj &&
+                     !(d->flags & KGE_FLAG_GRAD_ROWS_TOUCHED);   // (never write an untouched row)
   A.gent = d->grad_out[0];
   A.grel = d->grad_out[1];
   A.grel_aux = d->grad_out[2];
@@ -340,6 +341,28 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.pos_score_out = d->pos_score_out;
   A.neg_score_out = d->neg_score_out;
   A.norm2_out = d->norm2_out;
+  {
+    // split step (the multi-GPU sparse exchange): score pass, then update pass
+    const bool ps = d->flags & KGE_FLAG_PHASE_SCORE, pu = d->flags & KGE_FLAG_PHASE_UPDATE;
+    if (ps || pu) {
+      if (ps && pu) return fail(KGE_EINVAL, "KGE_FLAG_PHASE_SCORE and KGE_FLAG_PHASE_UPDATE are exclusive");
+      if (rescal || transr || proj)
+        return fail(KGE_EUNSUPPORTED, "the split step covers the element-wise family (TransE, DistMult, RotatE)");
+      if (d->optimizer != KGE_OPT_SGD) return fail(KGE_EINVAL, "the split step runs KGE_OPT_SGD");
+      if (!d->norm2_out || !d->grad_out[1])
+        return fail(KGE_EINVAL, "the split step needs norm2_out and grad_out[1] (relation gradients)");
+      if (fuse_norm_plan) return fail(KGE_EINVAL, "the split step needs KGE_FLAG_NO_TABLE_CONSTRAINT");
+    }
+    A.run_score = !pu;
+    A.run_update = !ps;
+    if (pu) {
+      A.scale_from_norm2 = true;
+      A.rel_grad = true;
+      A.grel = d->grad_out[1];
+      A.remote_from = d->remote_rows_from > 0 ? d->remote_rows_from : INT64_MAX;
+      A.abort_flag = d->abort_flag;
+    }
+  }
   A.status = d->status;
 
   uint64_t off = 0;
@@ -396,7 +419,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   {
     const int64_t f[] = {model, B, Keff, Kside, d->corrupt_side, E, R, entc, relc, rowlen, d->dim, d->dim_rel,
                          (int64_t)compact, cap, hbits, kshift, nWG, P.G.gridU, vec, ncp, wpp, SW, d->optimizer,
-                         d->flags, d->constraint, d->shard_count, (int64_t)P.ws_bytes,
+                         d->flags & ~(KGE_FLAG_PHASE_SCORE | KGE_FLAG_PHASE_UPDATE), d->constraint,
+                         d->shard_count, (int64_t)P.ws_bytes,
                          (int64_t)P.o_cnt, (int64_t)P.o_htab, (int64_t)P.o_coef, (int64_t)P.o_snap,
                          (int64_t)P.o_gpos, (int64_t)P.o_part, (int64_t)P.o_list, (int64_t)P.o_ovf,
                          (int64_t)P.o_upart, (int64_t)P.o_leaders, (int64_t)P.o_sorted, (int64_t)P.o_relseg,
@@ -447,6 +471,10 @@ __global__ __launch_bounds__(256) void apply_rows_kernel(float* __restrict__ w, 
 
 }  // namespace
 
+namespace kge {
+void kge_set_error(const char* msg) { g_err = msg; }
+}  // namespace kge
+
 extern "C" {
 
 kge_status kge_apply_rows(const kge_apply_rows_desc* d, void* stream) {
@@ -485,6 +513,7 @@ kge_status kge_apply(const kge_apply_desc* d, void* stream) {
   a.g = d->grad; a.norm2 = d->norm2; a.lr = d->lr; a.clip = d->clip_norm;
   a.adam = adam ? 1 : 0; a.m = d->m; a.v = d->v;
   a.b1 = d->beta_1; a.b2 = d->beta_2; a.eps = d->epsilon; a.lr_t = (float)lr_t;
+  a.abort = d->abort_flag;
   launch_apply(a, (hipStream_t)stream);
   return hip_check("kge_apply");
 }
@@ -629,6 +658,18 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   }
   hipEvent_t const* ev = (hipEvent_t const*)d->prof_events;
   if (ev) (void)hipEventRecord(ev[0], st);
+  const bool phase_update = d->flags & KGE_FLAG_PHASE_UPDATE;
+  if (phase_update) {
+    // the update pass alone (the score pass ran in the previous call): its
+    // relation gradients start from zero
+    if (d->batch > 0)
+      (void)hipMemsetAsync(d->grad_out[1], 0, (size_t)A.rel.rows * A.rel_gcols * sizeof(float), st);
+    if (ev) (void)hipEventRecord(ev[1], st);
+    if (d->batch > 0) s = launch_step_elementwise(A, P.G, d->model, P.sk, st, ev);
+    if (s != KGE_OK) return fail(s, "no kernel instance for model %d / score %d", d->model, P.sk);
+    if (ev) (void)hipEventRecord(ev[3], st);
+    return hip_check("kge_step(update pass)");
+  }
   const bool zero_ent = !(d->flags & KGE_FLAG_GRAD_ROWS_TOUCHED);
   // (RESCAL's dense passes write every row; so does a non-compact update
   // launch in grad mode, zeros for the untouched ones)

@@ -75,6 +75,9 @@ __device__ __forceinline__ bool ws_refused(StepCtl* ctl, uint32_t sig, int32_t* 
   return ws_refused_slow(ctl, s, sig, status, loss_out);
 }
 
+// sets the thread-local message kge_last_error() returns (kge_abi.hip)
+void kge_set_error(const char* msg);
+
 // Optimizer apply over a whole table (kge_apply, and the dense-gradient
 // steps' in-step SGD): clip_by_norm with the variable's norm^2, then SGD or
 // keras Adam (kge_hip.h kge_apply_desc). Guarded when launched by a step
@@ -85,6 +88,7 @@ struct ApplyArgs {
   float lr, clip;
   int adam; float* m; float* v; float b1, b2, eps, lr_t;
   StepCtl* ctl; uint32_t sig; int32_t* status;
+  const float* abort = nullptr;   // nonzero *abort: nothing applied
 };
 void launch_apply(const ApplyArgs& a, hipStream_t st);
 
@@ -186,6 +190,12 @@ struct StepArgs {
   float* norm2_out;
   int32_t* status;
   uint32_t sig;     // plan signature (ws_refused)
+  // split step (KGE_FLAG_PHASE_*, the multi-GPU sparse exchange)
+  bool run_score = true, run_update = true;
+  bool scale_from_norm2 = false;   // update pass: clip scales from norm2_out (all-reduced by the caller)
+  bool rel_grad = false;           // update pass: relation rows' raw gradients -> grel (no update)
+  int64_t remote_from = INT64_MAX; // entity rows >= this: raw gradient written in place of the row
+  const float* abort_flag = nullptr;   // update pass does nothing when *abort_flag != 0
 };
 
 struct StepGeom {

@@ -131,6 +131,7 @@ __device__ __forceinline__ void apply4(const ApplyArgs& a, float cs, float* w, c
 
 __global__ __launch_bounds__(256) void apply_kernel(ApplyArgs a, int flat4) {
   if (a.ctl && ws_refused(a.ctl, a.sig, a.status, nullptr)) return;
+  if (a.abort && *a.abort != 0.f) return;
   const float cs = a.clip / fmaxf(sqrtf(*a.norm2), a.clip);
   float dm = 0.f, dv = 0.f;
   if (flat4) {

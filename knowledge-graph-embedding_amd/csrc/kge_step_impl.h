@@ -875,7 +875,8 @@ void update_kernel(StepArgs A) {
   // workspace for this plan or refused it (and reported); here a refused
   // workspace just leaves every wave idle -- one scalar compare, no branch
   // of its own (an early return cost the compact instance registers)
-  const bool ws_ok = !KGE_GUARD_KU || *reinterpret_cast<const uint32_t*>(&A.ctl->plan_sig) == A.sig;
+  const bool ws_ok = (!KGE_GUARD_KU || *reinterpret_cast<const uint32_t*>(&A.ctl->plan_sig) == A.sig) &&
+                     !(A.abort_flag && *A.abort_flag != 0.f);   // (split step: a rank's exchange failed)
   if (A.compact) {   // one wave per key position: the destinations' first keys lead
     // (read unconditionally: the array is padded to the grid)
     const uint4 t = A.leaders[dd];
@@ -891,7 +892,11 @@ void update_kernel(StepArgs A) {
   const uint32_t nneg = A.nkeyneg;
   const uint32_t kmask = (1u << A.kshift) - 1u;
   const uint32_t snap_stride = (uint32_t)(M::NSNAP * A.snap_cols);   // B * stride < 2^32 (plan check)
-  const float sc_ent = A.ctl->scale[A.sc_ent_idx], sc_rel = A.ctl->scale[A.sc_rel_idx];   // issued up front
+  float sc_ent = A.ctl->scale[A.sc_ent_idx], sc_rel = A.ctl->scale[A.sc_rel_idx];   // issued up front
+  if (A.scale_from_norm2) {   // split step: the caller's (all-reduced) norms
+    sc_ent = -A.lr * (A.clip_norm / fmaxf(sqrtf(A.norm2_out[A.sc_ent_idx]), A.clip_norm));
+    sc_rel = -A.lr * (A.clip_norm / fmaxf(sqrtf(A.norm2_out[A.sc_rel_idx]), A.clip_norm));
+  }
 
   // one code -> its positive i and slot j (negative, c = -1) or row part c (0 h, 1 t, 2 r)
   auto decode = [&](uint32_t code, int64_t* i, int* j, int* c) {
@@ -1206,6 +1211,10 @@ void update_kernel(StepArgs A) {
         }
         if (A.grad_mode || A.dense) {
           store_row(acc, A.gent + d * (int64_t)A.ent.cols, A.ent.cols);
+        } else if (d >= A.remote_from) {
+          // a row fetched from its owner (split step): its raw summed
+          // gradient replaces it, and travels back to the owner
+          store_row(acc, A.ent.row_w(d), A.ent.cols);
         } else {
 #pragma unroll
           for (int q = 0; q < VEC * NC; ++q) E.v[q] = E.v[q] + acc.v[q] * sc_ent;
@@ -1213,7 +1222,7 @@ void update_kernel(StepArgs A) {
         }
       } else {
         const int64_t r = d - E_;
-        if (A.grad_mode) {
+        if (A.grad_mode || A.rel_grad) {
           store_rel_row<M::CPLX, VEC, NC>(racc, A.grel + r * (int64_t)A.rel_gcols, A.rel.cols);
         } else {
           float row[RV * NC];
@@ -1276,9 +1285,9 @@ static void launch_score(const StepArgs& A, const StepGeom& G, hipStream_t st) {
 
 template <template <int, int, int> class Model, int VEC, int NC, int SK>
 static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_t st, hipEvent_t const* ev) {
-  launch_score<Model, VEC, NC, SK>(A, G, st);
+  if (A.run_score) launch_score<Model, VEC, NC, SK>(A, G, st);
   if (ev) (void)hipEventRecord(ev[2], st);
-  if (A.train) {
+  if (A.train && A.run_update) {
     if constexpr (NC == 1 && !Model<VEC, NC, SK>::WIDE) {
       if (A.compact) {
         hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK, KGE_UPD_COMPACT_WPE>), dim3(G.gridU), dim3(kUpdThreads), 0,

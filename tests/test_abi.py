@@ -45,7 +45,8 @@ def _c_layout():
     from KGE import _hip
     structs = {"kge_table": _hip.kge_table, "kge_sampler_desc": _hip.kge_sampler_desc,
                "kge_sample_desc": _hip.kge_sample_desc, "kge_step_desc": _hip.kge_step_desc}
-    for extra in ("kge_apply_desc", "kge_rank_desc", "kge_apply_rows_desc", "kge_stream_desc"):
+    for extra in ("kge_apply_desc", "kge_rank_desc", "kge_apply_rows_desc", "kge_stream_desc", "kge_exchange_desc",
+                  "kge_exchange_rows_desc"):
         if hasattr(_hip, extra):
             structs[extra] = getattr(_hip, extra)
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "kge_hip.h"', 'int main(void){']

@@ -805,16 +805,18 @@ def test_fused_adam_three_steps(hiplib, model_name, constraint):
 
 
 @pytest.mark.parametrize("mode,model_name,score_kind",
-                         [(m, n, s) for m in ("sparse", "dense", "local")
+                         [(m, n, s) for m in ("sparse", "loopback", "dense", "local")
                           for n, s in (("TransE", "lp2"), ("TransD", "lppow2"), ("RotatE", "lp1"),
                                        ("TransR", "lppow2"), ("DistMult", None))]
                          + [("dense", "RESCAL", None), ("dense", "TransH", "lppow2")])
 def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
     """KGE/sharded.py on the RCCL backend (world size 1): e mod G shard,
-    kge_sample draws, the sparse (unique ids -> all_to_all ids / rows -> row
-    cache -> gradient rows back -> kge_apply_rows) or dense (all-gather /
-    reduce-scatter) exchange, grad-mode kge_step on the cache, all-reduce,
-    two steps == two oracle steps with the same draws."""
+    kge_sample draws, the device sparse exchange (kge_exchange_plan ->
+    fixed-capacity blocks -> split step or grad-mode step on the extended
+    table -> gradient rows back -> kge_exchange_rows; "loopback": every id
+    through the blocks, the remote path on one GPU) or the dense replica
+    (grad-mode step, one all-reduce, kge_apply); two steps == two oracle steps
+    with the same draws."""
     import torch.distributed as dist
     from KGE import loss, optimizers, score
     from KGE.ns_strategy import UniformStrategy
@@ -833,7 +835,8 @@ def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
         m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
         # "sparse" forces the exchange + row cache even on one rank; "local" is
         # the one-rank shortcut (the fused step directly on the shard)
-        st = ShardedStep(m, mode="sparse" if mode == "local" else mode, local_fast=mode == "local")
+        st = ShardedStep(m, mode="dense" if mode == "dense" else "sparse", local_fast=mode == "local",
+                         loopback=mode == "loopback")
         assert (st.direct is not None) == (mode == "local")
         ref_w = W
         opt = optimizers.SGD(0.05)
@@ -853,6 +856,81 @@ def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
         st.sync()
         for kk, v in ref_w.items():
             np.testing.assert_allclose(m.model_weights[kk].cpu().numpy(), v, atol=TOL, err_msg=kk)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model_name,loopback", [(n, lb) for n in ("TransE", "TransD") for lb in (False, True)])
+def test_sharded_sparse_adam_world1(hiplib, model_name, loopback):
+    """keras Adam through the device sparse exchange (world size 1): the
+    grad-mode step on the extended table, gradient rows accumulated by their
+    owner (kge_exchange_rows ACCUM), dense keras Adam over the shard -- three
+    steps == three oracle Adam steps."""
+    import torch.distributed as dist
+    from KGE import loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    from KGE.sharded import ShardedStep
+    dev = _dev()
+    _init_world1(dist, dev)
+    try:
+        rng = np.random.default_rng(31)
+        E, R, d, B, K = 41, 4, 24, 9, 6
+        k = 20 if model_name == "TransD" else None
+        W = _weights(model_name, E, R, d, rng, k)
+        sc = score.LpDistance(2) if model_name == "TransE" else score.LpDistancePow(2)
+        lf = loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0)
+        m = _make(model_name, d, K, "h+t", sc, lf, E, R, UniformStrategy(np.arange(E), seed=4), k=k)
+        m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
+        st = ShardedStep(m, mode="sparse", local_fast=False, loopback=loopback)
+        opt = optimizers.Adam(0.01)
+        ref_w, state = W, None
+        for it in range(3):
+            pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+            plane = m.ns_strategy.offset
+            lv = float(st(torch.tensor(pos, device=dev), True, opt))
+            torch.cuda.synchronize()
+            st.check_status()
+            neg = orc.negatives(pos, K, "h+t", E, seed=4, plane=plane)
+            ref = orc.train_step(model_name, ref_w, pos, neg, score=_spec_score(sc), loss=_spec_loss(lf), lr=0.01,
+                                 constraint=True, optimizer="adam", adam_state=state,
+                                 constraint_weight=getattr(m, "constraint_weight", 1.0))
+            ref_w, state = ref["weights"], ref["adam"]
+            assert abs(lv - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"])), it
+        st.sync()
+        for kk, v in ref_w.items():
+            np.testing.assert_allclose(m.model_weights[kk].cpu().numpy(), v, atol=TOL, err_msg=kk)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model_name", ["TransE", "TransR"])
+def test_sharded_exchange_overflow_voids_step(hiplib, model_name):
+    """A step whose ids overflow an owner block (capacity below the step's
+    unique ids) is skipped whole -- no table changes -- and check_status()
+    reports it; the next step with room runs normally."""
+    import torch.distributed as dist
+    from KGE import loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    from KGE.sharded import ShardedStep
+    dev = _dev()
+    _init_world1(dist, dev)
+    try:
+        rng = np.random.default_rng(37)
+        E, R, d, B, K = 300, 4, 24, 32, 8
+        k = 20 if model_name == "TransR" else None
+        W = _weights(model_name, E, R, d, rng, k)
+        m = _make(model_name, d, K, "h+t", score.LpDistancePow(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
+                  E, R, UniformStrategy(np.arange(E), seed=6), constraint=False, k=k)
+        m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
+        st = ShardedStep(m, mode="sparse", local_fast=False, loopback=True, capacity_slack=0.05, capacity_floor=0)
+        pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+        st(torch.tensor(pos, device=dev), True, optimizers.SGD(0.05))
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError, match="overflowed"):
+            st.check_status()
+        st.sync()
+        for kk, v in W.items():
+            np.testing.assert_array_equal(m.model_weights[kk].cpu().numpy(), v, err_msg=kk)
     finally:
         dist.destroy_process_group()
 
@@ -901,7 +979,8 @@ def test_gathered_shard_layout_remap(hiplib, model_name):
         np.testing.assert_allclose(got, v, atol=TOL, err_msg=kk)
 
 
-def test_sharded_step_c5_shard_size(hiplib):
+@pytest.mark.parametrize("loopback", [False, True])
+def test_sharded_step_c5_shard_size(hiplib, loopback):
     """One GPU at the C5 per-rank shard size (6.25M rows x 512, TransE, K=256
     h+t, SANS) through the sparse exchange: finite loss, only touched rows
     change, and the owner update equals the fused single-device step on the
@@ -925,7 +1004,8 @@ def test_sharded_step_c5_shard_size(hiplib):
             m = _make("TransE", d, K, "h+t", score.LpDistance(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
                       E, R, UniformStrategy(np.arange(E), seed=5), constraint=False)
             m.model_weights = {"ent_emb": ent.clone(), "rel_emb": rel.clone()}
-            stp = ShardedStep(m, mode="sparse", local_fast=False) if sharded else engine.FusedStep(m)
+            stp = ShardedStep(m, mode="sparse", local_fast=False, loopback=loopback) if sharded else \
+                engine.FusedStep(m)
             lv = float(stp(pos, True, optimizers.SGD(0.01)))
             torch.cuda.synchronize()
             stp.check_status()
