@@ -65,7 +65,9 @@ DENSE_TABLE_BYTES = 1 << 30   # "auto": replicated tables + one all-reduce below
 
 class Exchange:
     """The step's collectives on one process group (tensor forms on RCCL; the
-    gloo CPU tests of this logic get list forms with the same results)."""
+    gloo CPU tests of this logic get list forms with the same results). A
+    gloo group given device tensors stages them through host memory (the
+    multi-process tests that put several ranks on one GPU)."""
 
     def __init__(self, group=None):
         self.group = group
@@ -73,18 +75,31 @@ class Exchange:
         self.rank = dist.get_rank(group)
         self.tensor_forms = dist.get_backend(group) == "nccl"
 
+    def _host(self, t):
+        return t.cpu() if (not self.tensor_forms and t.is_cuda) else t
+
     def all_gather(self, full, shard):
         if self.tensor_forms:
             dist.all_gather_into_tensor(full, shard, group=self.group)
-        else:
-            dist.all_gather(list(full.chunk(self.world)), shard, group=self.group)
+            return
+        f = self._host(full)
+        dist.all_gather(list(f.chunk(self.world)), self._host(shard), group=self.group)
+        if f is not full:
+            full.copy_(f)
 
     def all_reduce(self, t):
-        if self.world > 1:   # (one rank: the sum is the tensor itself)
-            dist.all_reduce(t, group=self.group)
+        if self.world == 1:   # (one rank: the sum is the tensor itself)
+            return
+        h = self._host(t)
+        dist.all_reduce(h, group=self.group)
+        if h is not t:
+            t.copy_(h)
 
     def all_to_all(self, out, inp, out_splits=None, in_splits=None):
-        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+        o = self._host(out)
+        dist.all_to_all_single(o, self._host(inp.contiguous()), out_splits, in_splits, group=self.group)
+        if o is not out:
+            out.copy_(o)
 
 
 class ShardedStep:
