@@ -485,6 +485,10 @@ kge_status kge_sample(const kge_sample_desc* d, void* stream);
 
 /* Optimizer apply of one variable (see kge_apply_desc). */
 kge_status kge_apply(const kge_apply_desc* d, void* stream);
+/* n (<= 4) kge_apply calls in ONE launch -- a step's variables (ent / rel /
+ * rel_aux / ent_aux) after a multi-GPU reduction or a grad-mode step. Same
+ * result as the n calls in order; the variables must not overlap. */
+kge_status kge_apply_many(const kge_apply_desc* d, int32_t n, void* stream);
 
 /* Row constraints over a whole table (constraint.py:4-31, :70-99):
  * kind 0 = normalized_embeddings(p=2, value), 1 = clip_constraint(p=2, value).

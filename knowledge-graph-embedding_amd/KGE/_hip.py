@@ -134,7 +134,7 @@ class kge_stream_desc(ctypes.Structure):
 
 EXPORTS = ("kge_abi_version", "kge_last_error", "kge_step_workspace_bytes", "kge_step_plan_signature", "kge_step",
            "kge_sample",
-           "kge_apply", "kge_constrain_rows", "kge_rank", "kge_apply_rows", "kge_stream_batch", "kge_exchange_plan",
+           "kge_apply", "kge_apply_many", "kge_constrain_rows", "kge_rank", "kge_apply_rows", "kge_stream_batch", "kge_exchange_plan",
            "kge_exchange_rows")
 
 _lock = threading.Lock()
@@ -164,6 +164,8 @@ def load(path=LIB_PATH):
         L.kge_sample.argtypes = [ctypes.POINTER(kge_sample_desc), ctypes.c_void_p]
         L.kge_apply.restype = ctypes.c_int
         L.kge_apply.argtypes = [ctypes.POINTER(kge_apply_desc), ctypes.c_void_p]
+        L.kge_apply_many.restype = ctypes.c_int
+        L.kge_apply_many.argtypes = [ctypes.POINTER(kge_apply_desc), ctypes.c_int32, ctypes.c_void_p]
         L.kge_apply_rows.restype = ctypes.c_int
         L.kge_apply_rows.argtypes = [ctypes.POINTER(kge_apply_rows_desc), ctypes.c_void_p]
         L.kge_rank.restype = ctypes.c_int

@@ -337,9 +337,7 @@ class FusedStep:
             self.apply_adam(optimizer)
         return self.loss_out
 
-    def apply(self, var, grad, norm2_ptr, optimizer, name=None, abort=None):
-        """``kge_apply`` of one variable (SGD or keras Adam) with global norm^2
-        at ``norm2_ptr``; nothing applied when ``abort`` (device float [1]) is nonzero."""
+    def _apply_desc(self, var, grad, norm2_ptr, optimizer, name, abort):
         a = _hip.kge_apply_desc()
         if abort is not None:
             a.abort_flag = abort.data_ptr()
@@ -357,7 +355,22 @@ class FusedStep:
             a.iteration = optimizer.iterations
         else:
             a.optimizer = _hip.OPT_SGD
+        return a
+
+    def apply(self, var, grad, norm2_ptr, optimizer, name=None, abort=None):
+        """``kge_apply`` of one variable (SGD or keras Adam) with global norm^2
+        at ``norm2_ptr``; nothing applied when ``abort`` (device float [1]) is nonzero."""
+        a = self._apply_desc(var, grad, norm2_ptr, optimizer, name, abort)
         _hip.check(self.lib.kge_apply(a, _hip.stream_handle(self.device)), "kge_apply")
+
+    def apply_many(self, items, optimizer, abort=None):
+        """``kge_apply_many``: [(var, grad, norm2_ptr, name)] (up to 4) in one launch."""
+        items = [it for it in items if it[0].numel() > 0]
+        for i in range(0, len(items), 4):
+            chunk = items[i:i + 4]
+            arr = (_hip.kge_apply_desc * len(chunk))(*[self._apply_desc(v, g, n, optimizer, nm, abort)
+                                                       for v, g, n, nm in chunk])
+            _hip.check(self.lib.kge_apply_many(arr, len(chunk), _hip.stream_handle(self.device)), "kge_apply_many")
 
     def apply_adam(self, optimizer):
         optimizer.iterations += 1
@@ -365,8 +378,8 @@ class FusedStep:
         names = self.names or fused_names(self.model)
         g = self.grad_buffers()
         slot = {"ent": 0, "rel": 1, "rel_aux": 2, "ent_aux": 3}
-        for role, buf in zip(self.grad_roles(), g):
-            self.apply(t[role], buf, self.norm2.data_ptr() + 4 * slot[role], optimizer, names[role])
+        self.apply_many([(t[role], buf, self.norm2.data_ptr() + 4 * slot[role], names[role])
+                         for role, buf in zip(self.grad_roles(), g)], optimizer)
 
     def check_status(self):
         _hip.check_device_status(self.status, "kge_step")

@@ -462,11 +462,18 @@ class ShardedStep:
         else:
             _host_apply(var, grad, self.norm2[v], optimizer, name)
 
-    def _apply_rel(self, optimizer, abort=None):
+    def _apply_rel(self, optimizer, abort=None, extra=()):
+        """The replicated relation tables' apply (+ ``extra`` [(var, grad,
+        norm2 slot, name)]): one kge_apply_many launch on a GPU."""
         slot = {"rel": 1, "rel_aux": 2}
-        for r in self.rel_roles:
-            w = self.tables[r]
-            self._apply_dense(w.view(w.shape[0], -1), self.grel[r], slot[r], optimizer, self.names[r], abort=abort)
+        items = list(extra) + [(self.tables[r].view(self.tables[r].shape[0], -1), self.grel[r], slot[r], self.names[r])
+                               for r in self.rel_roles]
+        if self.fused is not None:
+            self.fused.apply_many([(v, g, self.norm2.data_ptr() + 4 * k, n) for v, g, k, n in items], optimizer,
+                                  abort=abort)
+            return
+        for v, g, k, n in items:
+            self._apply_dense(v, g, k, optimizer, n, abort=abort)
 
     # ------------------------------------------------------------ step
     def __call__(self, batch, is_train, optimizer, neg_ids=None, prof_events=None):
@@ -489,10 +496,9 @@ class ShardedStep:
                     g1 = gbuf.reshape(-1)
                     self.norm2[slot:slot + 1].copy_(torch.dot(g1, g1).reshape(1))
             if is_train:
-                for k, gk in enumerate(self.gent):
-                    self._apply_dense(self._ent_rows(k), gk, self._slot(k), optimizer,
-                                      self.names["ent" if k == 0 else "ent_aux"])
-                self._apply_rel(optimizer)
+                ents = [(self._ent_rows(k), gk, self._slot(k), self.names["ent" if k == 0 else "ent_aux"])
+                        for k, gk in enumerate(self.gent)]
+                self._apply_rel(optimizer, extra=ents)   # every variable in one launch
             return self.loss
         if neg_ids is None:
             neg_ids = self._draw(batch)
@@ -692,6 +698,7 @@ class ShardedStep:
         # 4. the fetched rows' gradients back to their owners; owners apply
         # them source by source in rank order (SGD) or add them up (Adam: a
         # dense keras Adam of the shard)
+        dense_items = []
         if G > 1 or loop:
             adam = isinstance(optimizer, _opt.Adam)
             for k, gk in enumerate(grad_blocks):
@@ -706,14 +713,13 @@ class ShardedStep:
                     acc = torch.zeros(self.Es, cols, dtype=torch.float32, device=self.device)
                     for s in range(G):
                         self._xrows(b, _hip.XROWS_ACCUM, gk, gk.stride(0), view, source=s, acc=acc)
-                    self._apply_dense(view[:self.valid], acc[:self.valid], self._slot(k), optimizer,
-                                      self._shard_name(k), abort=small[-1:])
+                    dense_items.append((view[:self.valid], acc[:self.valid], self._slot(k), self._shard_name(k)))
                 else:
                     for s in range(G):
                         self._xrows(b, _hip.XROWS_SGD, gk, gk.stride(0), view, source=s,
                                     norm2_ptr=self.norm2.data_ptr() + 4 * self._slot(k),
                                     lr=optimizer.learning_rate)
-        self._apply_rel(optimizer, abort=small[-1:])
+        self._apply_rel(optimizer, abort=small[-1:], extra=dense_items)
         return self.loss
 
     def _gblocks(self, b):

@@ -492,21 +492,21 @@ kge_status kge_apply_rows(const kge_apply_rows_desc* d, void* stream) {
   return hip_check("kge_apply_rows");
 }
 
-kge_status kge_apply(const kge_apply_desc* d, void* stream) {
-  if (!d) return fail(KGE_EINVAL, "null descriptor");
+static kge_status apply_args(const kge_apply_desc* d, ApplyArgs* out, const char* who) {
+  if (!d) return fail(KGE_EINVAL, "%s: null descriptor", who);
   const kge_table& t = d->var;
-  if (!t.data || t.rows < 0 || t.cols <= 0 || t.ld < t.cols) return fail(KGE_EINVAL, "kge_apply: bad table");
+  if (!t.data || t.rows < 0 || t.cols <= 0 || t.ld < t.cols) return fail(KGE_EINVAL, "%s: bad table", who);
   if (d->optimizer != KGE_OPT_SGD && d->optimizer != KGE_OPT_ADAM)
-    return fail(KGE_EINVAL, "kge_apply: optimizer must be KGE_OPT_SGD or KGE_OPT_ADAM");
-  if (!d->grad || !d->norm2) return fail(KGE_EINVAL, "kge_apply: null grad / norm2");
-  if (!(d->clip_norm > 0.f)) return fail(KGE_EINVAL, "kge_apply: clip_norm must be > 0");
+    return fail(KGE_EINVAL, "%s: optimizer must be KGE_OPT_SGD or KGE_OPT_ADAM", who);
+  if (!d->grad || !d->norm2) return fail(KGE_EINVAL, "%s: null grad / norm2", who);
+  if (!(d->clip_norm > 0.f)) return fail(KGE_EINVAL, "%s: clip_norm must be > 0", who);
   const bool adam = d->optimizer == KGE_OPT_ADAM;
   double lr_t = 0.0;
   if (adam) {
-    if (!d->m || !d->v) return fail(KGE_EINVAL, "kge_apply: Adam needs m and v slots");
-    if (d->iteration < 1) return fail(KGE_EINVAL, "kge_apply: Adam iteration must be >= 1");
-    const double t = (double)d->iteration;
-    lr_t = (double)d->lr * std::sqrt(1.0 - std::pow((double)d->beta_2, t)) / (1.0 - std::pow((double)d->beta_1, t));
+    if (!d->m || !d->v) return fail(KGE_EINVAL, "%s: Adam needs m and v slots", who);
+    if (d->iteration < 1) return fail(KGE_EINVAL, "%s: Adam iteration must be >= 1", who);
+    const double it = (double)d->iteration;
+    lr_t = (double)d->lr * std::sqrt(1.0 - std::pow((double)d->beta_2, it)) / (1.0 - std::pow((double)d->beta_1, it));
   }
   ApplyArgs a{};
   a.w = t.data; a.rows = t.rows; a.cols = (int32_t)t.cols; a.ld = t.ld;
@@ -514,8 +514,28 @@ kge_status kge_apply(const kge_apply_desc* d, void* stream) {
   a.adam = adam ? 1 : 0; a.m = d->m; a.v = d->v;
   a.b1 = d->beta_1; a.b2 = d->beta_2; a.eps = d->epsilon; a.lr_t = (float)lr_t;
   a.abort = d->abort_flag;
+  *out = a;
+  return KGE_OK;
+}
+
+kge_status kge_apply(const kge_apply_desc* d, void* stream) {
+  ApplyArgs a;
+  const kge_status s = apply_args(d, &a, "kge_apply");
+  if (s != KGE_OK) return s;
   launch_apply(a, (hipStream_t)stream);
   return hip_check("kge_apply");
+}
+
+kge_status kge_apply_many(const kge_apply_desc* d, int32_t n, void* stream) {
+  if (n < 0 || n > kMaxApply) return fail(KGE_EINVAL, "kge_apply_many: n must be in [0, %d]", kMaxApply);
+  if (n > 0 && !d) return fail(KGE_EINVAL, "kge_apply_many: null descriptor array");
+  ApplyArgs a[kMaxApply];
+  for (int i = 0; i < n; ++i) {
+    const kge_status s = apply_args(d + i, &a[i], "kge_apply_many");
+    if (s != KGE_OK) return s;
+  }
+  launch_apply_many(a, n, (hipStream_t)stream);
+  return hip_check("kge_apply_many");
 }
 
 kge_status kge_stream_batch(const kge_stream_desc* d, void* stream) {

@@ -91,6 +91,9 @@ struct ApplyArgs {
   const float* abort = nullptr;   // nonzero *abort: nothing applied
 };
 void launch_apply(const ApplyArgs& a, hipStream_t st);
+// up to kMaxApply variables in one launch (blocks split between them by size)
+constexpr int kMaxApply = 4;
+void launch_apply_many(const ApplyArgs* a, int n, hipStream_t st);
 
 // Everything a step kernel needs, passed by value (kernarg segment).
 struct StepArgs {

@@ -129,21 +129,21 @@ __device__ __forceinline__ void apply4(const ApplyArgs& a, float cs, float* w, c
   }
 }
 
-__global__ __launch_bounds__(256) void apply_kernel(ApplyArgs a, int flat4) {
+__device__ __forceinline__ void apply_body(const ApplyArgs& a, int flat4, int64_t blk, int64_t nblk) {
   if (a.ctl && ws_refused(a.ctl, a.sig, a.status, nullptr)) return;
   if (a.abort && *a.abort != 0.f) return;
   const float cs = a.clip / fmaxf(sqrtf(*a.norm2), a.clip);
   float dm = 0.f, dv = 0.f;
   if (flat4) {
     const int64_t n4 = a.rows * (int64_t)a.cols / 4;
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (int64_t)gridDim.x * blockDim.x)
+    for (int64_t q = blk * blockDim.x + threadIdx.x; q < n4; q += nblk * blockDim.x)
       apply4(a, cs, a.w + 4 * q, a.g + 4 * q, a.adam ? a.m + 4 * q : nullptr, a.adam ? a.v + 4 * q : nullptr);
     return;
   }
   const bool v4 = a.cols % 4 == 0 && a.ld % 4 == 0 && ((uintptr_t)a.w % 16) == 0 && ((uintptr_t)a.g % 16) == 0 &&
                   (!a.adam || (((uintptr_t)a.m % 16) == 0 && ((uintptr_t)a.v % 16) == 0));
-  const int64_t nw = (int64_t)gridDim.x * (blockDim.x / KGE_WAVE);
-  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x / KGE_WAVE) + wave_id(); r < a.rows; r += nw) {
+  const int64_t nw = nblk * (blockDim.x / KGE_WAVE);
+  for (int64_t r = blk * (blockDim.x / KGE_WAVE) + wave_id(); r < a.rows; r += nw) {
     float* wr = a.w + r * a.ld;
     const int64_t go = r * (int64_t)a.cols;
     if (v4) {
@@ -156,15 +156,44 @@ __global__ __launch_bounds__(256) void apply_kernel(ApplyArgs a, int flat4) {
   }
 }
 
-void launch_apply(const ApplyArgs& a, hipStream_t st) {
-  const int64_t total = a.rows * (int64_t)a.cols;
-  if (total == 0) return;
-  const bool flat4 = a.ld == a.cols && total % 4 == 0 && ((uintptr_t)a.w % 16) == 0 && ((uintptr_t)a.g % 16) == 0 &&
-                     (!a.adam || (((uintptr_t)a.m % 16) == 0 && ((uintptr_t)a.v % 16) == 0));
-  const int64_t work = flat4 ? (total / 4 + 255) / 256 : (a.rows + 3) / 4;
-  const unsigned blocks = (unsigned)std::min<int64_t>(std::max<int64_t>(work, 1), 8192);
-  hipLaunchKernelGGL(apply_kernel, dim3(blocks), dim3(256), 0, st, a, flat4 ? 1 : 0);
+struct ApplyMany {
+  ApplyArgs a[kMaxApply];
+  int32_t flat4[kMaxApply];
+  uint32_t first[kMaxApply + 1];   // variable v owns blocks [first[v], first[v + 1])
+  int32_t n;
+};
+
+__global__ __launch_bounds__(256) void apply_kernel(ApplyMany M) {
+  const uint32_t b = blockIdx.x;
+  int v = 0;
+  while (v + 1 < M.n && b >= M.first[v + 1]) ++v;
+  apply_body(M.a[v], M.flat4[v], (int64_t)(b - M.first[v]), (int64_t)(M.first[v + 1] - M.first[v]));
 }
+
+void launch_apply_many(const ApplyArgs* a, int n, hipStream_t st) {
+  ApplyMany M{};
+  uint32_t nb = 0;
+  int k = 0;
+  for (int i = 0; i < n && i < kMaxApply; ++i) {
+    const int64_t total = a[i].rows * (int64_t)a[i].cols;
+    if (total == 0) continue;
+    const bool flat4 = a[i].ld == a[i].cols && total % 4 == 0 && ((uintptr_t)a[i].w % 16) == 0 &&
+                       ((uintptr_t)a[i].g % 16) == 0 &&
+                       (!a[i].adam || (((uintptr_t)a[i].m % 16) == 0 && ((uintptr_t)a[i].v % 16) == 0));
+    const int64_t work = flat4 ? (total / 4 + 255) / 256 : (a[i].rows + 3) / 4;
+    M.a[k] = a[i];
+    M.flat4[k] = flat4 ? 1 : 0;
+    M.first[k] = nb;
+    nb += (uint32_t)std::min<int64_t>(std::max<int64_t>(work, 1), 8192);
+    ++k;
+  }
+  if (k == 0) return;
+  M.first[k] = nb;
+  M.n = k;
+  hipLaunchKernelGGL(apply_kernel, dim3(nb), dim3(256), 0, st, M);
+}
+
+void launch_apply(const ApplyArgs& a, hipStream_t st) { launch_apply_many(&a, 1, st); }
 
 kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int model, int sk,
                                    hipStream_t st, hipEvent_t const* ev) {
