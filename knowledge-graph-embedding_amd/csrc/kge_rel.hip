@@ -132,30 +132,29 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
   const int ti = (int)(blockIdx.x % nct), i0 = ti * 16;
   const int lane = lane_id(), wv = wave_id();
   float* Xc = sm;             // [32][16]
-  float* Yc = sm + 32 * 16;   // [16][D16]
+  float* Yc = sm + 32 * 16;   // [32][D16]
   __shared__ const float* s_x[32];
   __shared__ const float* s_y[32];
   __shared__ float s_n2[4], s_m2[4];
   // the strip's rows [i0, i0 + 16) are one contiguous run of 16 d floats in
-  // both R_r and dR_r: its R_r part (<= 4 float4 per thread, d <= 256) is
-  // requested first, under the list lookup and the MFMA loop
+  // both R_r and dR_r
   const int run = min(16, d - i0) * d;
   const float* Rm = P.rel.row(r) + (int64_t)i0 * d;
   const bool v4 = d % 4 == 0 && P.rel.ld % 4 == 0 && ((uintptr_t)P.rel.p % 16) == 0 && ((uintptr_t)P.grel % 16) == 0;
   constexpr int kRunV = 16 * 256 / 4 / 256;
-  float4 m[kRunV];
-#pragma unroll
-  for (int k = 0; k < kRunV; ++k) {
-    const int e = 4 * (threadIdx.x + k * 256);
-    m[k] = (v4 && e < run) ? *reinterpret_cast<const float4*>(Rm + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
   const int64_t beg = P.rel_beg[r], end = beg + P.rel_cnt[r];
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // staged rows: every load of a chunk issued before any is stored (a float4
+  // per lane when the rows allow) -- one L2 round trip per chunk, where a
+  // scalar load-store loop took ~13 and made this pass 47 us at C4
+  const bool vy = d % 4 == 0 && P.ent.ld % 4 == 0 && P.gcols % 4 == 0 && ((uintptr_t)P.ent.p % 16) == 0 &&
+                  ((uintptr_t)P.gpos % 16) == 0;
+  constexpr int kYV = 8;   // float4 per thread: 8 threads x 8 float4 cover a row (D16 <= 256)
   for (int64_t c0 = beg; c0 < end; c0 += 16) {
     const int nrow = (int)min<int64_t>(16, end - c0);
-    __syncthreads();
+    __syncthreads();   // the previous chunk's MFMA reads of Xc / Yc
     if (threadIdx.x < 32) {   // each staged row's source, resolved once: h | b rows, A | t rows
       const int q = threadIdx.x & 15;
       const int64_t i = q < nrow ? P.sorted[c0 + q] : 0;
@@ -169,29 +168,45 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
       }
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < 32 * 16; e += blockDim.x) {
-      const int q = e >> 4, c = i0 + (e & 15);
-      Xc[e] = ((q & 15) < nrow && c < d) ? s_x[q][c] : 0.f;
+    float xv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = threadIdx.x + u * 256, q = e >> 4, c = i0 + (e & 15);
+      xv[u] = ((q & 15) < nrow && c < d) ? s_x[q][c] : 0.f;
     }
-    // Y in two halves through one [16][D16] buffer (A rows for k < 16, then
-    // t rows): half the LDS, so twice the workgroups per CU; same k order
+    if (vy) {   // 8 threads per staged row (one row pointer each), float4 columns 32 apart
+      const int q = threadIdx.x >> 3, l8 = threadIdx.x & 7;
+      const float* src = s_y[q];
+      const bool live = (q & 15) < nrow;
+      float4 yv[kYV];
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      if (half) __syncthreads();   // the first half's MFMA reads of Yc
-      for (int e = threadIdx.x; e < 16 * D16; e += blockDim.x) {
-        const int q = e / D16, c = e - q * D16;
-        Yc[e] = (q < nrow && c < d) ? s_y[16 * half + q][c] : 0.f;
+      for (int u = 0; u < kYV; ++u) {
+        const int c = 4 * (l8 + 8 * u);
+        yv[u] = (live && c < d) ? *reinterpret_cast<const float4*>(src + c) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      __syncthreads();
 #pragma unroll
-      for (int k0 = 0; k0 < 16; k0 += 4) {
-        const int k = k0 + (lane >> 4);
-        const float a = Xc[(16 * half + k) * 16 + (lane & 15)];
+      for (int u = 0; u < kYV; ++u) {
+        const int c = 4 * (l8 + 8 * u);
+        if (c < D16) *reinterpret_cast<float4*>(Yc + q * D16 + c) = yv[u];
+      }
+    } else {
+      for (int e = threadIdx.x; e < 32 * D16; e += blockDim.x) {
+        const int q = e / D16, c = e - q * D16;
+        Yc[e] = ((q & 15) < nrow && c < d) ? s_y[q][c] : 0.f;
+      }
+    }
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int jt = wv + 4 * t;
-          if (jt < nct) acc[t] = mfma16(a, Yc[k * D16 + jt * 16 + (lane & 15)], acc[t]);
-        }
+    for (int u = 0; u < 2; ++u) Xc[threadIdx.x + u * 256] = xv[u];
+    __syncthreads();
+    // k = 0..15: h_i with A_i, k = 16..31: b_i with t_i (positive order)
+#pragma unroll 1
+    for (int k0 = 0; k0 < 32; k0 += 4) {
+      const int k = k0 + (lane >> 4);
+      const float a = Xc[k * 16 + (lane & 15)];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int jt = wv + 4 * t;
+        if (jt < nct) acc[t] = mfma16(a, Yc[k * D16 + jt * 16 + (lane & 15)], acc[t]);
       }
     }
   }
@@ -199,10 +214,18 @@ __global__ __launch_bounds__(256) void rel_dr_kernel(RelArgs P) {
   // per lane. Relations absent from the batch (most workgroups) have no
   // MFMA part: their strip is dense_rel * R_r -- not even written when the
   // apply pass re-derives it (lazy_absent: the norm partials only)
+  // the strip's R_r part (<= 4 float4 per thread, d <= 256), loaded after the
+  // loop: live across it, its 16 registers cost the pass half its occupancy
+  float4 m[kRunV];
+#pragma unroll
+  for (int k = 0; k < kRunV; ++k) {
+    const int e = 4 * (threadIdx.x + k * 256);
+    m[k] = (v4 && e < run) ? *reinterpret_cast<const float4*>(Rm + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   const bool absent = beg == end;
   const bool store = !(absent && P.lazy_absent);
   float* G = P.grel + r * (int64_t)d * d + (int64_t)i0 * d;
-  float* S = Yc;   // [16][D16]
+  float* S = Yc;   // [16][D16] of the [32][D16] image
   if (!absent) {
     __syncthreads();   // the MFMA loop's last reads of Yc
 #pragma unroll
@@ -268,14 +291,24 @@ __global__ __launch_bounds__(256) void rescal_norms_kernel(RelArgs P, int nr, co
   __shared__ float s_w[4][4];
   const int lane = lane_id(), wv = wave_id();
   float a[4] = {0.f, 0.f, 0.f, 0.f};   // rel grad^2 | ||R||^2 | ent grad^2 | ||e||^2
-  for (int w = threadIdx.x; w < nr; w += blockDim.x) {
-    a[0] += P.rpart[w];
-    a[1] += P.rpart[nr + w];
-  }
-  for (int w = threadIdx.x; w < nu; w += blockDim.x) {
-    a[2] += upart[w];
-    a[3] += upart[nu + w];
-  }
+  // eight partials of each sum in flight per thread (a serial load-add chain
+  // of ~25 L2 round trips made this one-workgroup pass ~10 us); fixed order
+  constexpr int U = 8;
+  auto sum2 = [&](const float* x, int n, float& s0, float& s1) {
+    for (int w0 = threadIdx.x; w0 < n; w0 += U * blockDim.x) {
+      float q0[U], q1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int w = w0 + u * blockDim.x;
+        q0[u] = w < n ? x[w] : 0.f;
+        q1[u] = w < n ? x[n + w] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) { s0 += q0[u]; s1 += q1[u]; }
+    }
+  };
+  sum2(P.rpart, nr, a[0], a[1]);
+  sum2(upart, nu, a[2], a[3]);
 #pragma unroll
   for (int k = 0; k < 4; ++k) a[k] = wave_sum(a[k]);
   if (lane == 0) {
@@ -458,7 +491,7 @@ void launch_rescal_apply(const RelArgs& P, const TabView& ent, const float* gent
 void launch_rel_post(const RelArgs& P, hipStream_t st) {
   // (g_h, g_t: the score kernel's waves, Rescal::SELF_CTX)
   const int nct = (P.d + 15) / 16;
-  const size_t lds2 = (32 * 16 + 16 * (size_t)nct * 16) * sizeof(float);
+  const size_t lds2 = (32 * 16 + 32 * (size_t)nct * 16) * sizeof(float);
   hipLaunchKernelGGL(rel_dr_kernel, dim3((unsigned)(P.rel.rows * nct)), dim3(256), lds2, st, P);
 }
 void launch_reg_loss(const TabView& ent, const TabView& rel, float lam, float* part, StepCtl* ctl,

@@ -18,6 +18,9 @@ static kge_status rescal_vn(const StepArgs& A, const StepGeom& G, const RelArgs&
   if (lam != 0.f && !A.train) launch_reg_loss(A.ent, A.rel, lam, regpart, A.ctl, A.loss_out, A.loss_accum, A.sig, A.status, st);
   if (ev) (void)hipEventRecord(ev[2], st);
   if (A.train) {
+    // (the dR pass and the dense entity update are independent, but a second
+    // stream costs more than it overlaps: ~11 us per cross-queue event wait,
+    // measured, profiles/r03/rescal_side_stream.txt)
     launch_rel_post(P, st);   // dR strips: dense relation gradient + norm^2 / ||R||^2 partials
     hipLaunchKernelGGL((update_kernel<Rescal, VEC, NC, SK_DOT>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
     // both dense norms, the regulariser loss term, the SGD scales
