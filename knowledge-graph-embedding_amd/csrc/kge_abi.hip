@@ -265,7 +265,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     if (d->flags & KGE_FLAG_DEBUG_LIST_CAP) cap = 4;
   }
   const int64_t nlists = compact ? (1LL << hbits) : ndest;
-  const int64_t nupd = compact ? T : ndest;
+  const int64_t nupd = compact ? ceil_div(T, kUpdKeysPerWave) : ndest;   // compact: waves of kUpdKeysPerWave keys
   P.G.gridU = (int)ceil_div(nupd, kUpdWaves);
   P.rescal = rescal;
   P.transr = transr;
@@ -379,7 +379,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.o_list = take((uint64_t)nlists * cap * 4);
   P.o_ovf = take((uint64_t)T * 8);
   P.o_upart = take((uint64_t)P.G.gridU * 2 * 4);   // gradient norm^2 | entity norm^2 (dense mode)
-  P.o_leaders = take((uint64_t)(compact ? (int64_t)P.G.gridU * kUpdWaves : 1) * 16);
+  P.o_leaders = take((uint64_t)(compact ? (int64_t)P.G.gridU * kUpdWaves * kUpdKeysPerWave : 1) * 16);
   P.hbits = hbits;
   if (rescal) {
     const int64_t nct = ceil_div(d->dim, 16);

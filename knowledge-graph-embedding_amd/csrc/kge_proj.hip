@@ -129,7 +129,10 @@ __global__ __launch_bounds__(256) void transh_dense_kernel(StepArgs A, PjPlan J)
 
 template <int VEC, int NC>
 static void upd_mat(const StepArgs& A, unsigned grid, hipStream_t st) {
-  hipLaunchKernelGGL((update_kernel<Materialised, VEC, NC, SK_DOT>), dim3(grid), dim3(kUpdThreads), 0, st, A);
+  if (A.compact)
+    hipLaunchKernelGGL((update_kernel<Materialised, VEC, NC, SK_DOT, 1, true>), dim3(grid), dim3(kUpdThreads), 0, st, A);
+  else
+    hipLaunchKernelGGL((update_kernel<Materialised, VEC, NC, SK_DOT>), dim3(grid), dim3(kUpdThreads), 0, st, A);
 }
 static void launch_update_mat_pj(const StepArgs& A, int vec, int nc, unsigned grid, hipStream_t st) {
   if (grid == 0) return;
@@ -180,7 +183,8 @@ kge_status launch_step_proj(const StepArgs& A, const StepGeom& G, const PjPlan& 
     // compact: their leaders are positives' keys, the first 3B positions
     B2.rel_only = true;
     if (A.compact) {
-      grid2 = (unsigned)((A.npos3 + kUpdWaves - 1) / kUpdWaves);
+      const int64_t waves = (A.npos3 + kUpdKeysPerWave - 1) / kUpdKeysPerWave;
+      grid2 = (unsigned)((waves + kUpdWaves - 1) / kUpdWaves);
     } else {
       grid2 = (unsigned)((A.rel.rows + kUpdWaves - 1) / kUpdWaves);
     }

@@ -12,6 +12,10 @@ constexpr int kStepWaves = KGE_STEP_WAVES;
 constexpr int kStepThreads = kStepWaves * KGE_WAVE;
 constexpr int kUpdWaves = 4;       // waves per update workgroup (one destination row per wave)
 constexpr int kUpdThreads = kUpdWaves * KGE_WAVE;
+#ifndef KGE_UPD_KR
+#define KGE_UPD_KR 4               // compact update launch: key positions per wave (tuning knob)
+#endif
+constexpr int kUpdKeysPerWave = KGE_UPD_KR;
 constexpr int kMaxWpp = kStepWaves > 8 ? kStepWaves : 8;   // waves per positive, at most
 #ifndef KGE_SLOTS_PER_WAVE
 #define KGE_SLOTS_PER_WAVE 64      // score kernel: negative slots a wave streams, at most (tuning knob)
@@ -276,20 +280,32 @@ constexpr int kTrWaves = 8;
 constexpr int kTrThreads = kTrWaves * KGE_WAVE;
 constexpr int kTrMaxSlots = 72;   // K + 1 slots over 8 waves, 9 per wave in registers
 constexpr int kTrMaxDim = 256;    // d, k (MFMA k-steps held in registers)
+// GEMM1 / GEMM2 inner dimensions run over NC whole 16-column chunks, a
+// compile-time count (straight-line MFMA code, B columns in 4*NC registers):
+// the smallest of 4, 8, 13, 16 covering max(d, k)
+__host__ __device__ inline int tr_nc(int d, int k) {
+  const int c = ((d > k ? d : k) + 15) / 16;
+  return c <= 4 ? 4 : c <= 8 ? 8 : c <= 13 ? 13 : 16;
+}
 // LDS carve of the TransR kernel (floats): X [NR16][LX] | P [NR16][LP], later
-// S [SR16][LP] over both; then per-row / per-slot scalars and partials
+// S [SR16][LP] over both; then per-row / per-slot scalars and partials.
+// Rows are W = 16 NC floats (zero past d / k) plus 4: the stride mod 32 banks
+// is 4 or 20, so the 8 rows served together by a ds_read_b128 operand fetch
+// hit disjoint bank quads.
 struct TrLds {
-  int LX, LP, NR16, SR16;
+  int NC, W, LX, LP, NR16, SR16;
   int pn, xx, xh, xt, sS, sR, sT, sA, rp, ids, misc, total_floats;
 };
 __host__ __device__ inline TrLds tr_lds(int d, int k, int K) {
   TrLds L;
-  L.LX = ((d + 15) & ~15) + 1;   // rows padded to whole 16-column MFMA chunks (zero), odd stride
-  L.LP = ((k + 15) & ~15) + 1;
+  L.NC = tr_nc(d, k);
+  L.W = 16 * L.NC;
+  L.LX = L.W + 4;
+  L.LP = L.W + 4;
   L.NR16 = (K + 2 + 15) & ~15;
   L.SR16 = (2 * K + 4 + 15) & ~15;
   int o = L.NR16 * (L.LX + L.LP);
-  if (L.SR16 * L.LP + 16 > o) o = L.SR16 * L.LP + 16;   // + slack: GEMM3 reads whole 16-column tiles
+  if (L.SR16 * L.LP > o) o = L.SR16 * L.LP;
   L.pn = o; o += L.NR16;
   L.xx = o; o += L.NR16;
   L.xh = o; o += L.NR16;

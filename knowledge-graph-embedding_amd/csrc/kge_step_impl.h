@@ -846,7 +846,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
 // chain wants occupancy more than it minds 16 spilled registers in the
 // long-list paths (C2-50M KU 189 -> 172 us); the full launch keeps the
 // allocator's choice (71 registers, 7 waves), 2 % faster at C2.
-template <template <int, int, int> class Model, int VEC, int NC, int SK, int UW = 1>
+template <template <int, int, int> class Model, int VEC, int NC, int SK, int UW = 1, bool CMP = false>
 __global__ __launch_bounds__(kUpdThreads) __attribute__((amdgpu_waves_per_eu(UW)))
 void update_kernel(StepArgs A) {
   using M = Model<VEC, NC, SK>;
@@ -868,27 +868,12 @@ void update_kernel(StepArgs A) {
   const int64_t R_ = A.rel_dests ? A.rel.rows : 0;
   const int64_t ndest = E_ + R_;
   const int64_t dd = (int64_t)blockIdx.x * kUpdWaves + wv;
-  int64_t d, li;   // destination row, its list index (the row, or its hash slot)
-  bool active;
-  uint32_t code1 = 0xFFFFFFFFu;   // compact: the destination's first filed code
   // workspace guard (ws_refused): the step's first kernel claimed the
   // workspace for this plan or refused it (and reported); here a refused
   // workspace just leaves every wave idle -- one scalar compare, no branch
   // of its own (an early return cost the compact instance registers)
   const bool ws_ok = (!KGE_GUARD_KU || *reinterpret_cast<const uint32_t*>(&A.ctl->plan_sig) == A.sig) &&
                      !(A.abort_flag && *A.abort_flag != 0.f);   // (split step: a rank's exchange failed)
-  if (A.compact) {   // one wave per key position: the destinations' first keys lead
-    // (read unconditionally: the array is padded to the grid)
-    const uint4 t = A.leaders[dd];
-    active = ws_ok && dd < (int64_t)A.nkeys && t.y != 0xFFFFFFFFu && !(A.rel_only && (int64_t)t.x < E_);
-    d = active ? (int64_t)t.x : 0;
-    li = active ? (int64_t)t.z : 0;
-    code1 = t.y;
-  } else {
-    active = ws_ok && dd < (A.rel_only ? R_ : ndest);
-    d = dd < R_ ? E_ + dd : dd - R_;
-    li = d;
-  }
   const uint32_t nneg = A.nkeyneg;
   const uint32_t kmask = (1u << A.kshift) - 1u;
   const uint32_t snap_stride = (uint32_t)(M::NSNAP * A.snap_cols);   // B * stride < 2^32 (plan check)
@@ -980,25 +965,28 @@ void update_kernel(StepArgs A) {
 
   float dn2 = 0.f;   // dense mode: this wave's ||summed row gradient||^2
   float en2 = 0.f;   // dense mode: this wave's ||entity row||^2 (the regulariser loss, RESCAL.py:190-198)
+  // one destination row d (list index li; compact: code1 = its first filed code)
+  auto run_dest = [&](const int64_t d, const int64_t li, const uint32_t code1, const bool active) {
+  accE = 0.f;
   if (active) {
     const bool is_ent = d < E_;
     const uint32_t* lst = A.list + li * (int64_t)A.cap;
     // issued together: the counter, the list's first 64 entries (speculative;
     // lanes past the count are ignored) and the entity row
-    const uint32_t n = A.compact ? (uint32_t)A.htab[li] : A.cnt[d];
+    const uint32_t n = CMP ? (uint32_t)A.htab[li] : A.cnt[d];
     // list entry q (compact launches: position 0 is the leader's code1, and
     // the list is read only once the count says there is more than one key)
-    const bool l0 = KGE_COMPACT_LIST0 && A.compact;
+    const bool l0 = KGE_COMPACT_LIST0 && CMP;
     auto lst_at = [&](uint32_t q) -> uint32_t { return (l0 && q == 0u) ? code1 : lst[q]; };
     uint32_t code0 = 0xFFFFFFFFu;
-    if (!A.compact) code0 = lst[min(lane, A.cap - 1)];   // speculative: issued with the counter
+    if (!CMP) code0 = lst[min(lane, A.cap - 1)];   // speculative: issued with the counter
     F E, acc;
     acc.zero();
     E.zero();
     // compact launches over large tables: most destinations hold exactly one
     // key, whose code came with the destination -- its coefficient and context
     // row are requested together with the counter (used when n == 1)
-    const bool pre = A.compact && is_ent && code1 < nneg;
+    const bool pre = CMP && is_ent && code1 < nneg;
     typename M::ECtx ec1;
     float2 cf1 = make_float2(0.f, 0.f);
     int kd1 = 0;
@@ -1014,7 +1002,7 @@ void update_kernel(StepArgs A) {
     // an untouched row is read only when the step rewrites it anyway (fused
     // constraint) or it carries a dense term; a compact launch visits only
     // touched rows (issued without waiting for the counter)
-    if (is_ent && (A.compact || n != 0u || A.fuse_norm || A.dense)) {
+    if (is_ent && (CMP || n != 0u || A.fuse_norm || A.dense)) {
       load_row(E, A.ent.row(d), A.ent.cols);
       if (A.fuse_norm) {
         normalize_row(E);   // the step's constraint assign, then this step's update
@@ -1024,7 +1012,7 @@ void update_kernel(StepArgs A) {
     }
     if (n != 0u || (A.dense && is_ent)) {
       if (lane == 0 && n != 0u && !A.keep_cnt) {   // ready for the next step
-        if (A.compact) A.htab[li] = 0ull;
+        if (CMP) A.htab[li] = 0ull;
         else A.cnt[d] = 0u;
       }
       float racc[RV * NC];
@@ -1095,7 +1083,7 @@ void update_kernel(StepArgs A) {
       } else if (n <= (uint32_t)A.cap && n <= (uint32_t)KGE_WAVE) {
         // ascending code order: each code's rank among the n (codes are
         // unique), then a forward permute puts code of rank r in lane r
-        if (A.compact) code0 = lane < (int)n ? lst_at((uint32_t)lane) : 0xFFFFFFFFu;
+        if (CMP) code0 = lane < (int)n ? lst_at((uint32_t)lane) : 0xFFFFFFFFu;
         const uint32_t code = lane < (int)n ? code0 : 0xFFFFFFFFu;
         uint32_t rank = 0u;
         for (int q = 0; q < (int)n; ++q) rank += ((uint32_t)__builtin_amdgcn_readlane((int)code, q) < code) ? 1u : 0u;
@@ -1243,6 +1231,90 @@ void update_kernel(StepArgs A) {
       }
     }
   }
+  };
+
+  if constexpr (CMP) {
+    // KR key positions per wave: the destinations' first keys lead. Every
+    // position's leader entry, then for the common case at large tables -- an
+    // entity row holding exactly one (negative) key, whose code came with the
+    // destination -- the counter, coefficient, context row and entity row of
+    // all KR are requested together (KR times the bytes in flight of one
+    // destination per wave: the launch is latency-bound). Those rows are
+    // finished here with the arithmetic of run_dest's single-key case; every
+    // other destination goes through run_dest. (Leaders are read
+    // unconditionally: the array is padded to the grid.)
+    constexpr int KR = kUpdKeysPerWave;
+    const bool one_ok = !A.dense && !A.grad_mode;
+    uint4 t[KR];
+    bool act[KR], one[KR];
+    uint32_t n1[KR];
+    F E1[KR];
+    typename M::ECtx c1[KR];
+    float2 f1[KR];
+    static_for<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      t[r] = A.leaders[dd * KR + r];
+    });
+    static_for<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      act[r] = ws_ok && dd * KR + r < (int64_t)A.nkeys && t[r].y != 0xFFFFFFFFu &&
+               !(A.rel_only && (int64_t)t[r].x < E_);
+      one[r] = one_ok && act[r] && (int64_t)t[r].x < E_ && t[r].y < nneg;
+      n1[r] = 0u;
+      f1[r] = make_float2(0.f, 0.f);
+      E1[r].zero();
+      if (one[r]) {
+        n1[r] = (uint32_t)A.htab[t[r].z];
+        if constexpr (M::MAT) {
+          load_row(c1[r].c0, A.gneg + (int64_t)t[r].y * A.ent.cols, A.ent.cols);
+        } else {
+          f1[r] = A.coef[t[r].y];
+          M::load_ectx(A.snap + (t[r].y >> A.kshift) * snap_stride, A.snap_cols,
+                       slot_kind(A.side_mode, (int)(t[r].y & kmask)), c1[r]);
+        }
+        load_row(E1[r], A.ent.row(t[r].x), A.ent.cols);
+      }
+    });
+    static_for<KR>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if (one[r] && n1[r] == 1u) {
+        const int64_t d = (int64_t)t[r].x;
+        F E = E1[r], acc;
+        acc.zero();
+        if (A.fuse_norm) normalize_row(E);
+        if (lane == 0 && !A.keep_cnt) A.htab[t[r].z] = 0ull;
+        const int kd = slot_kind(A.side_mode, (int)(t[r].y & kmask));
+        if constexpr (M::LINEAR_E) {
+          float aE, aC;
+          M::lin_coefs(kd, f1[r].x, aE, aC);
+          const float sE = 0.f + aE;
+#pragma unroll
+          for (int q = 0; q < VEC * NC; ++q) acc.v[q] += aC * c1[r].c0.v[q];
+#pragma unroll
+          for (int q = 0; q < VEC * NC; ++q) acc.v[q] += sE * E.v[q];
+        } else {
+          F g;
+          M::grad_entity(c1[r], kd, E, f1[r].x, f1[r].y, g);
+          add_to(acc, g);
+        }
+        if (d >= A.remote_from) {
+          store_row(acc, A.ent.row_w(d), A.ent.cols);
+        } else {
+#pragma unroll
+          for (int q = 0; q < VEC * NC; ++q) E.v[q] = E.v[q] + acc.v[q] * sc_ent;
+          store_row(E, A.ent.row_w(d), A.ent.cols);
+        }
+        act[r] = false;
+      }
+    });
+#pragma unroll
+    for (int r = 0; r < KR; ++r)
+      if (act[r]) run_dest((int64_t)t[r].x, (int64_t)t[r].z, t[r].y, true);
+  } else {
+    const bool active = ws_ok && dd < (A.rel_only ? R_ : ndest);
+    const int64_t d = dd < R_ ? E_ + dd : dd - R_;
+    run_dest(d, d, 0xFFFFFFFFu, active);
+  }
   if (A.dense) {
     // ||dense gradient||^2: workgroup partial; partials_norm_kernel (the next
     // launch) sums them in a fixed order (clip_by_norm of the dense tensor) --
@@ -1288,12 +1360,13 @@ static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_
   if (A.run_score) launch_score<Model, VEC, NC, SK>(A, G, st);
   if (ev) (void)hipEventRecord(ev[2], st);
   if (A.train && A.run_update) {
-    if constexpr (NC == 1 && !Model<VEC, NC, SK>::WIDE) {
-      if (A.compact) {
-        hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK, KGE_UPD_COMPACT_WPE>), dim3(G.gridU), dim3(kUpdThreads), 0,
-                           st, A);
-        return KGE_OK;
-      }
+    if (A.compact) {
+      if constexpr (NC == 1 && !Model<VEC, NC, SK>::WIDE)
+        hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK, KGE_UPD_COMPACT_WPE, true>), dim3(G.gridU),
+                           dim3(kUpdThreads), 0, st, A);
+      else
+        hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK, 1, true>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
+      return KGE_OK;
     }
     hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
   }

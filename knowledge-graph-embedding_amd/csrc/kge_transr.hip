@@ -39,7 +39,6 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 
 constexpr int kTrQ = (kTrMaxSlots + kTrWaves - 1) / kTrWaves;   // slots per wave
 constexpr int kTrKV = kTrMaxDim / KGE_WAVE;                     // projected-row floats per lane
-constexpr int kTrKS = kTrMaxDim / 4;                            // MFMA k-steps held in registers
 constexpr int kTrKS3 = ((kTrMaxSlots + 1 + 15) / 16) * 4;       // GEMM3 k-steps (K + 2 slot rows, 16-padded)
 
 // element gradient of the score wrt a = x - y (Lp kinds): score_grad's rule
@@ -56,33 +55,31 @@ __device__ __forceinline__ float lp_elem_grad(float a, float alpha, float M) {
 __device__ __forceinline__ float wsum(float x) { return lane_reduce<5, false>(x); }
 __device__ __forceinline__ float wmax(float x) { return lane_reduce<5, true>(x); }
 
-// Two 16x16 output tiles sharing one B column (bf, in registers): A rows from
-// LDS at p0 / p1 (lane-adjusted: row l & 15, k offset l >> 4), 16 columns
-// (4 k-steps) per chunk, the chunk's A values read before its MFMAs so one
-// LDS wait covers 8 MFMAs, and two independent accumulator chains. Pad
-// columns of A and padded k-steps of bf are zero.
-template <int KS>
-__device__ __forceinline__ void mfma_pair_lds_a(f32x4& a0, f32x4& a1, const float* p0, const float* p1,
-                                                const float (&bf)[KS], int nkc) {
+// Two 16x16 output tiles sharing one B column (bf, in registers) over NC
+// 16-wide k chunks, straight-line. The k order inside a chunk is permuted so
+// each lane's four A values are adjacent: MFMA step u of chunk c gives lane
+// group g = l >> 4 the index k = 16c + 4g + u (bf is loaded in the same
+// order), so A comes from LDS as ONE ds_read_b128 per tile per chunk. p0 / p1
+// point at row (l & 15) of each tile plus 4g; pad columns of A and bf are zero.
+template <int NC>
+__device__ __forceinline__ void mfma_pair_b128(f32x4& a0, f32x4& a1, const float* p0, const float* p1,
+                                               const float (&bf)[4 * NC]) {
 #pragma unroll
-  for (int c = 0; c < KS / 4; ++c) {
-    if (c < nkc) {
-      float x0[4], x1[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        x0[u] = p0[(c * 4 + u) * 4];
-        x1[u] = p1[(c * 4 + u) * 4];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a0 = mfma16(x0[u], bf[c * 4 + u], a0);
-        a1 = mfma16(x1[u], bf[c * 4 + u], a1);
-      }
-    }
+  for (int c = 0; c < NC; ++c) {
+    const float4 x0 = *reinterpret_cast<const float4*>(p0 + 16 * c);
+    const float4 x1 = *reinterpret_cast<const float4*>(p1 + 16 * c);
+    a0 = mfma16(x0.x, bf[4 * c + 0], a0);
+    a1 = mfma16(x1.x, bf[4 * c + 0], a1);
+    a0 = mfma16(x0.y, bf[4 * c + 1], a0);
+    a1 = mfma16(x1.y, bf[4 * c + 1], a1);
+    a0 = mfma16(x0.z, bf[4 * c + 2], a0);
+    a1 = mfma16(x1.z, bf[4 * c + 2], a1);
+    a0 = mfma16(x0.w, bf[4 * c + 3], a0);
+    a1 = mfma16(x1.w, bf[4 * c + 3], a1);
   }
 }
 
-template <int SK>
+template <int SK, int NC>
 __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   __shared__ float s_w[kTrWaves][4];
@@ -90,7 +87,8 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
   if (ws_refused(A.ctl, A.sig, A.status, A.loss_out)) return;
   const int d = T.d, k = T.k, K = A.Keff, NR = K + 2, NS = 2 * K + 4;
   const TrLds L = tr_lds(d, k, K);
-  const int LX = L.LX, LP = L.LP, D4 = LX - 1, K4 = LP - 1;
+  constexpr int W = 16 * NC;   // padded row width (L.W)
+  const int LX = L.LX, LP = L.LP, g4 = 4 * (lane_id() >> 4);
   float* X = sm;
   float* P = sm + L.NR16 * LX;
   float* S = sm;   // over X and P once both are consumed
@@ -141,7 +139,7 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
 #pragma unroll
       for (int c4 = 0; c4 < kTrKV; ++c4) {
         const int c = lane + KGE_WAVE * c4;
-        if (c < D4) X[row * LX + c] = v[u][c4];
+        if (c < W) X[row * LX + c] = v[u][c4];
       }
     }
   }
@@ -165,32 +163,34 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
   // ---- GEMM1: P = X M_r  (wave = 16-column tile of P; row tiles in pairs)
   const float* Mr = T.proj.row(pr);
   {
-    const int nct = (k + 15) / 16, nkc = (LX - 1) / 16, nrt = L.NR16 / 16;
+    const int nct = (k + 15) / 16, nrt = L.NR16 / 16;
     // jobs = (column tile, row-tile pair), column-major, dealt to the waves in
     // equal contiguous ranges (13 column tiles over 8 waves left two SIMDs
     // with a third more work); B is reloaded only when the column tile changes
     const int npr = (nrt + 1) / 2, nj = nct * npr;
     const int jb = wv * nj / kTrWaves, je = (wv + 1) * nj / kTrWaves;
     int cur = -1;
-    float bf[kTrKS];
+    float bf[4 * NC];
     for (int jo = jb; jo < je; ++jo) {
       const int ct = jo / npr, rt = (jo - ct * npr) * 2;
       const int col = ct * 16 + (lane & 15);
       if (ct != cur) {
         cur = ct;
 #pragma unroll
-        for (int ks = 0; ks < kTrKS; ++ks) {
-          const int kk = ks * 4 + (lane >> 4);
-          bf[ks] = (kk < d && col < k) ? Mr[(int64_t)kk * k + col] : 0.f;
-        }
+        for (int c = 0; c < NC; ++c)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int kk = 16 * c + g4 + u;
+            bf[4 * c + u] = (kk < d && col < k) ? Mr[(int64_t)kk * k + col] : 0.f;
+          }
       }
       {
         const int rt1 = rt + 1 < nrt ? rt + 1 : rt;   // odd count: the last tile twice (discarded)
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-        const float* x0 = X + (rt * 16 + (lane & 15)) * LX + (lane >> 4);
-        const float* x1 = X + (rt1 * 16 + (lane & 15)) * LX + (lane >> 4);
-        mfma_pair_lds_a(a0, a1, x0, x1, bf, nkc);
-        if (col < K4) {
+        const float* x0 = X + (rt * 16 + (lane & 15)) * LX + g4;
+        const float* x1 = X + (rt1 * 16 + (lane & 15)) * LX + g4;
+        mfma_pair_b128<NC>(a0, a1, x0, x1, bf);
+        if (col < W) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             P[(rt * 16 + (lane >> 4) * 4 + g) * LP + col] = a0[g];
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
 #pragma unroll
       for (int v = 0; v < kTrKV; ++v) {
         const int c = lane + KGE_WAVE * v;
-        if (c < K4) {
+        if (c < W) {
           S[r0 * LP + c] = G[m][0][v];
           S[r1 * LP + c] = G[m][1][v];
         }
@@ -419,14 +419,14 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
 #pragma unroll
     for (int v = 0; v < kTrKV; ++v) {
       const int c = lane + KGE_WAVE * v;
-      if (c < K4) rp[wv * LP + c] = rsum[v];
+      if (c < W) rp[wv * LP + c] = rsum[v];
     }
     for (int e = tid; e < (L.SR16 - NS) * LP; e += kTrThreads) S[NS * LP + e] = 0.f;
     __syncthreads();
     // summed positive rows, in slot order (deterministic): h = pos + tc slices,
     // t = pos + hc slices; r = the waves' partial sums in wave order
     float* gp = A.gpos + i * 3 * (int64_t)A.gcols;
-    for (int c = tid; c < K4; c += kTrThreads) {
+    for (int c = tid; c < W; c += kTrThreads) {
       float h = S[(K + 2) * LP + c], t = S[(K + 3) * LP + c];
       for (int q = 0; q < K; ++q) {
         const float v = S[(K + 4 + q) * LP + c];
@@ -443,30 +443,49 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
     KGE_PROF(39);
     // ---- GEMM2: Y = S M_r^T -> entity-row gradients and slice norms
     {
-      const int nct = (d + 15) / 16, nkc = (LP - 1) / 16, nrt = (NS + 15) / 16;
+      const int nct = (d + 15) / 16, nrt = (NS + 15) / 16;
       float* gp2 = gp;
       // (column tile, row-tile pair) jobs in equal contiguous ranges, as GEMM1
       const int npr = (nrt + 1) / 2, nj = nct * npr;
       const int jb = wv * nj / kTrWaves, je = (wv + 1) * nj / kTrWaves;
+      // B = M_r^T: lane (column l & 15, group g) reads M_r row `col` at
+      // 16c + 4g .. +3 -- one float4 per chunk when rows are 16-byte aligned
+      const bool mv4 = (k & 3) == 0 && (T.proj.ld & 3) == 0 && ((uintptr_t)T.proj.p & 15) == 0;
       int cur = -1;
-      float bf[kTrKS];
+      float bf[4 * NC];
       for (int jo = jb; jo < je; ++jo) {
         const int ct = jo / npr, rt = (jo - ct * npr) * 2;
         const int col = ct * 16 + (lane & 15);
         if (ct != cur) {
           cur = ct;
+          const float* mrow = Mr + (int64_t)col * k;
+          if (mv4) {
 #pragma unroll
-          for (int ks = 0; ks < kTrKS; ++ks) {
-            const int kk = ks * 4 + (lane >> 4);
-            bf[ks] = (kk < k && col < d) ? Mr[(int64_t)col * k + kk] : 0.f;
+            for (int c = 0; c < NC; ++c) {
+              const int kk = 16 * c + g4;
+              float4 m4 = make_float4(0.f, 0.f, 0.f, 0.f);
+              if (kk < k && col < d) m4 = *reinterpret_cast<const float4*>(mrow + kk);
+              bf[4 * c + 0] = m4.x;
+              bf[4 * c + 1] = m4.y;
+              bf[4 * c + 2] = m4.z;
+              bf[4 * c + 3] = m4.w;
+            }
+          } else {
+#pragma unroll
+            for (int c = 0; c < NC; ++c)
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const int kk = 16 * c + g4 + u;
+                bf[4 * c + u] = (kk < k && col < d) ? mrow[kk] : 0.f;
+              }
           }
         }
         {
           const int rt1 = rt + 1 < nrt ? rt + 1 : rt;
           f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-          const float* s0 = S + (rt * 16 + (lane & 15)) * LP + (lane >> 4);
-          const float* s1 = S + (rt1 * 16 + (lane & 15)) * LP + (lane >> 4);
-          mfma_pair_lds_a(acc[0], acc[1], s0, s1, bf, nkc);
+          const float* s0 = S + (rt * 16 + (lane & 15)) * LP + g4;
+          const float* s1 = S + (rt1 * 16 + (lane & 15)) * LP + g4;
+          mfma_pair_b128<NC>(acc[0], acc[1], s0, s1, bf);
           if (col < d) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -654,8 +673,14 @@ __global__ __launch_bounds__(256) void transr_proj_apply(StepArgs A, TrArgs T) {
 }
 
 static void launch_update_mat(const StepArgs& A, const StepGeom& G, hipStream_t st) {
-#define KGE_UPD(V, N) \
-  hipLaunchKernelGGL((update_kernel<Materialised, V, N, SK_DOT>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A)
+#define KGE_UPD(V, N)                                                                                            \
+  do {                                                                                                           \
+    if (A.compact)                                                                                               \
+      hipLaunchKernelGGL((update_kernel<Materialised, V, N, SK_DOT, 1, true>), dim3(G.gridU), dim3(kUpdThreads), 0, \
+                         st, A);                                                                                 \
+    else                                                                                                         \
+      hipLaunchKernelGGL((update_kernel<Materialised, V, N, SK_DOT>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A); \
+  } while (0)
   if (G.vec == 4) {
     if (G.nc == 1) KGE_UPD(4, 1); else if (G.nc == 2) KGE_UPD(4, 2); else KGE_UPD(4, 4);
   } else {
@@ -669,7 +694,14 @@ static void launch_tr(const StepArgs& A, const StepGeom& G, const TrArgs& T, con
                       hipEvent_t const* ev) {
   if (A.train) launch_rel_rank(P, st);
   const TrLds L = tr_lds(T.d, T.k, A.Keff);
-  hipLaunchKernelGGL(transr_kernel<SK>, dim3((unsigned)A.B), dim3(kTrThreads), (size_t)L.total_floats * 4, st, A, T);
+  const dim3 grid((unsigned)A.B), blk(kTrThreads);
+  const size_t lds = (size_t)L.total_floats * 4;
+  switch (L.NC) {
+    case 4: hipLaunchKernelGGL((transr_kernel<SK, 4>), grid, blk, lds, st, A, T); break;
+    case 8: hipLaunchKernelGGL((transr_kernel<SK, 8>), grid, blk, lds, st, A, T); break;
+    case 13: hipLaunchKernelGGL((transr_kernel<SK, 13>), grid, blk, lds, st, A, T); break;
+    default: hipLaunchKernelGGL((transr_kernel<SK, 16>), grid, blk, lds, st, A, T); break;
+  }
   if (ev) (void)hipEventRecord(ev[2], st);
   if (A.train) {
     launch_update_mat(A, G, st);

@@ -26,7 +26,7 @@ PHASES = {32: "ids", 33: "gather X", 34: "row stats + GEMM1", 35: "clip", 36: "s
 
 def build():
     objs, procs = [], []
-    for src in ("kge_step.hip", "kge_abi.hip", "kge_transr.hip", "kge_rel.hip", "kge_stream.hip"):
+    for src in ("kge_step.hip", "kge_abi.hip", "kge_transr.hip", "kge_rel.hip", "kge_stream.hip", "kge_exchange.hip"):
         obj = os.path.join("/tmp", "trprof_" + src.replace(".hip", ".o"))
         cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DKGE_PHASE_PROF", "-DKGE_ONLY_ONE",
                "-c", os.path.join(CSRC, src), "-o", obj]
