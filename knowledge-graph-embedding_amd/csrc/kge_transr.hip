@@ -79,6 +79,23 @@ __device__ __forceinline__ void mfma_pair_b128(f32x4& a0, f32x4& a1, const float
   }
 }
 
+// One 16x16 tile (the odd last row tile of a GEMM): the same k order, the
+// chunk's four steps split over two accumulator chains (added at the end) so
+// the 40-cycle dependent MFMA latency stays under the 32-cycle issue interval
+template <int NC>
+__device__ __forceinline__ void mfma_one_b128(f32x4& a0, const float* p0, const float (&bf)[4 * NC]) {
+  f32x4 b0 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const float4 x0 = *reinterpret_cast<const float4*>(p0 + 16 * c);
+    a0 = mfma16(x0.x, bf[4 * c + 0], a0);
+    b0 = mfma16(x0.y, bf[4 * c + 1], b0);
+    a0 = mfma16(x0.z, bf[4 * c + 2], a0);
+    b0 = mfma16(x0.w, bf[4 * c + 3], b0);
+  }
+  a0 += b0;
+}
+
 template <int SK, int NC>
 __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -185,11 +202,12 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
           }
       }
       {
-        const int rt1 = rt + 1 < nrt ? rt + 1 : rt;   // odd count: the last tile twice (discarded)
+        const int rt1 = rt + 1 < nrt ? rt + 1 : rt;   // odd count: the last tile alone
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
         const float* x0 = X + (rt * 16 + (lane & 15)) * LX + g4;
         const float* x1 = X + (rt1 * 16 + (lane & 15)) * LX + g4;
-        mfma_pair_b128<NC>(a0, a1, x0, x1, bf);
+        if (rt1 != rt) mfma_pair_b128<NC>(a0, a1, x0, x1, bf);
+        else mfma_one_b128<NC>(a0, x0, bf);
         if (col < W) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
@@ -485,7 +503,8 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
           f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
           const float* s0 = S + (rt * 16 + (lane & 15)) * LP + g4;
           const float* s1 = S + (rt1 * 16 + (lane & 15)) * LP + g4;
-          mfma_pair_b128<NC>(acc[0], acc[1], s0, s1, bf);
+          if (rt1 != rt) mfma_pair_b128<NC>(acc[0], acc[1], s0, s1, bf);
+          else mfma_one_b128<NC>(acc[0], s0, bf);
           if (col < d) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -535,21 +554,37 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
           f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
           const float* b0 = S + (lane >> 4) * LP + ct * 16 + (lane & 15);
           const float* b1 = S + (lane >> 4) * LP + ct1 * 16 + (lane & 15);
+          if (ct1 != ct) {
 #pragma unroll
-          for (int c = 0; c < kTrKS3 / 4; ++c) {
-            if (c < nkc) {
-              float y0[4], y1[4];
+            for (int c = 0; c < kTrKS3 / 4; ++c) {
+              if (c < nkc) {
+                float y0[4], y1[4];
 #pragma unroll
-              for (int u = 0; u < 4; ++u) {
-                y0[u] = b0[(c * 4 + u) * 4 * LP];
-                y1[u] = b1[(c * 4 + u) * 4 * LP];
-              }
+                for (int u = 0; u < 4; ++u) {
+                  y0[u] = b0[(c * 4 + u) * 4 * LP];
+                  y1[u] = b1[(c * 4 + u) * 4 * LP];
+                }
 #pragma unroll
-              for (int u = 0; u < 4; ++u) {
-                a0 = mfma16(af[c * 4 + u], y0[u], a0);
-                a1 = mfma16(af[c * 4 + u], y1[u], a1);
+                for (int u = 0; u < 4; ++u) {
+                  a0 = mfma16(af[c * 4 + u], y0[u], a0);
+                  a1 = mfma16(af[c * 4 + u], y1[u], a1);
+                }
               }
             }
+          } else {   // the odd last column tile alone: two chains, added
+#pragma unroll
+            for (int c = 0; c < kTrKS3 / 4; ++c) {
+              if (c < nkc) {
+                float y0[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) y0[u] = b0[(c * 4 + u) * 4 * LP];
+                a0 = mfma16(af[c * 4 + 0], y0[0], a0);
+                a1 = mfma16(af[c * 4 + 1], y0[1], a1);
+                a0 = mfma16(af[c * 4 + 2], y0[2], a0);
+                a1 = mfma16(af[c * 4 + 3], y0[3], a1);
+              }
+            }
+            a0 += a1;
           }
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
