@@ -134,7 +134,8 @@ class kge_stream_desc(ctypes.Structure):
 
 EXPORTS = ("kge_abi_version", "kge_last_error", "kge_step_workspace_bytes", "kge_step_plan_signature", "kge_step",
            "kge_sample",
-           "kge_apply", "kge_apply_many", "kge_constrain_rows", "kge_rank", "kge_apply_rows", "kge_stream_batch", "kge_exchange_plan",
+           "kge_apply", "kge_apply_many", "kge_constrain_rows", "kge_rank", "kge_apply_rows", "kge_stream_batch",
+           "kge_stream_permutation", "kge_stream_batch_perm", "kge_exchange_plan",
            "kge_exchange_rows")
 
 _lock = threading.Lock()
@@ -172,6 +173,12 @@ def load(path=LIB_PATH):
         L.kge_rank.argtypes = [ctypes.POINTER(kge_rank_desc), ctypes.c_void_p]
         L.kge_stream_batch.restype = ctypes.c_int
         L.kge_stream_batch.argtypes = [ctypes.POINTER(kge_stream_desc), ctypes.c_void_p]
+        L.kge_stream_permutation.restype = ctypes.c_int
+        L.kge_stream_permutation.argtypes = [ctypes.POINTER(kge_stream_desc), ctypes.c_int64, ctypes.c_void_p,
+                                             ctypes.c_void_p]
+        L.kge_stream_batch_perm.restype = ctypes.c_int
+        L.kge_stream_batch_perm.argtypes = [ctypes.POINTER(kge_stream_desc), ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_int64, ctypes.c_void_p]
         L.kge_exchange_plan.restype = ctypes.c_int
         L.kge_exchange_plan.argtypes = [ctypes.POINTER(kge_exchange_desc), ctypes.c_void_p]
         L.kge_exchange_rows.restype = ctypes.c_int

@@ -137,8 +137,11 @@ class DeviceBatcher:
     batches straddle epochs like ``repeat().batch()``. ``pi_e`` is a fresh
     permutation per epoch when shuffling (``reshuffle_each_iteration``): the
     stateless Philox-keyed Feistel permutation of ``kge_stream_desc``
-    (``include/kge_hip.h``), computed per output row on the GPU by
-    ``kge_stream_batch`` -- no permutation array, no host work per batch. On a
+    (``include/kge_hip.h``). On the GPU each epoch's permutation is
+    materialised once (``kge_stream_permutation``, int32 [n]) and a batch is a
+    gather through it (``kge_stream_batch_perm``); ``kge_stream_batch``
+    computes the same rows per output row without the table (tiny sets whose
+    batch spans more than two epochs). No host work per batch. On a
     CPU device the same rows come from the numpy restatement in
     ``_philox.stream_rows``. tf.data's buffered shuffle order itself is not
     reproducible (TF is not installed); the stream semantics are.
@@ -167,6 +170,8 @@ class DeviceBatcher:
         self.reuse_buffer = bool(reuse_buffer)
         self._desc = None
         self._out = None
+        self._perms = {}   # epoch -> its materialised permutation (device int32 [n])
+        self._spare = []
 
     def __iter__(self):
         return self
@@ -203,8 +208,28 @@ class DeviceBatcher:
                 self._dref = ctypes.byref(d)
             d.start = start
             d.out = out.data_ptr()
-            stream = torch.cuda.current_stream(self.data.device).cuda_stream
-            _hip.check(L.kge_stream_batch(self._dref, ctypes.c_void_p(stream)), "kge_stream_batch")
+            stream = ctypes.c_void_p(torch.cuda.current_stream(self.data.device).cuda_stream)
+            if self.shuffle and B <= self.n and self.n <= 2 ** 31 - 1:
+                # each epoch's permutation materialised once (kge_stream_permutation),
+                # the batch gathered through it: the same rows as kge_stream_batch
+                # without a per-batch cycle walk
+                e0, e1 = start // self.n, (start + B - 1) // self.n
+                perms = self._perms
+                for e in list(perms):
+                    if e < e0:   # (reused on this stream: stream order keeps it safe)
+                        self._spare.append(perms.pop(e))
+                for e in (e0, e1):
+                    if e not in perms:
+                        t = self._spare.pop() if self._spare else torch.empty(self.n, dtype=torch.int32,
+                                                                                device=self.data.device)
+                        _hip.check(L.kge_stream_permutation(self._dref, e, ctypes.c_void_p(t.data_ptr()), stream),
+                                   "kge_stream_permutation")
+                        perms[e] = t
+                _hip.check(L.kge_stream_batch_perm(self._dref, ctypes.c_void_p(perms[e0].data_ptr()),
+                                                   ctypes.c_void_p(perms[e1].data_ptr()), e0, stream),
+                           "kge_stream_batch_perm")
+                return out
+            _hip.check(L.kge_stream_batch(self._dref, stream), "kge_stream_batch")
             return out
         idx = torch.from_numpy(self.rows(start, B))
         return self.data.index_select(0, idx)

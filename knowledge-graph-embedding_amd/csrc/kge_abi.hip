@@ -556,6 +556,43 @@ kge_status kge_stream_batch(const kge_stream_desc* d, void* stream) {
   return hip_check("kge_stream_batch");
 }
 
+static kge_status stream_check(const kge_stream_desc* d, const char* fn) {
+  if (!d) return fail(KGE_EINVAL, "null descriptor");
+  if (d->abi_version != KGE_ABI_VERSION)
+    return fail(KGE_EINVAL, "abi_version %d != library %d", d->abi_version, KGE_ABI_VERSION);
+  if (d->n_rows <= 0) return fail(KGE_EINVAL, "%s: n_rows must be > 0 (empty triple set)", fn);
+  if (d->n_rows > INT32_MAX) return fail(KGE_ERANGE, "%s: n_rows exceeds 2^31 - 1 (int32 permutation)", fn);
+  return KGE_OK;
+}
+
+kge_status kge_stream_permutation(const kge_stream_desc* d, int64_t epoch, int32_t* perm, void* stream) {
+  if (kge_status s = stream_check(d, "kge_stream_permutation")) return s;
+  if (epoch < 0) return fail(KGE_EINVAL, "kge_stream_permutation: epoch must be >= 0");
+  if (!perm) return fail(KGE_EINVAL, "kge_stream_permutation: null perm");
+  if (d->shuffle != 1) return fail(KGE_EINVAL, "kge_stream_permutation: shuffle must be 1 (epoch order needs none)");
+  launch_stream_perm(d->n_rows, d->seed, epoch, perm, (hipStream_t)stream);
+  return hip_check("kge_stream_permutation");
+}
+
+kge_status kge_stream_batch_perm(const kge_stream_desc* d, const int32_t* perm_lo, const int32_t* perm_hi,
+                                 int64_t epoch_lo, void* stream) {
+  if (kge_status s = stream_check(d, "kge_stream_batch_perm")) return s;
+  if (d->idx_dtype != KGE_IDX_I32 && d->idx_dtype != KGE_IDX_I64)
+    return fail(KGE_EINVAL, "kge_stream_batch_perm: idx_dtype must be KGE_IDX_I32 or KGE_IDX_I64");
+  if (d->start < 0 || d->batch < 0) return fail(KGE_EINVAL, "kge_stream_batch_perm: start and batch must be >= 0");
+  if (d->batch == 0) return KGE_OK;
+  if (d->start > INT64_MAX - d->batch) return fail(KGE_ERANGE, "kge_stream_batch_perm: stream position overflows");
+  if (!d->triples || !d->out || !perm_lo) return fail(KGE_EINVAL, "kge_stream_batch_perm: null triples / out / perm_lo");
+  const int64_t e0 = d->start / d->n_rows, e1 = (d->start + d->batch - 1) / d->n_rows;
+  if (e0 != epoch_lo || e1 > epoch_lo + 1)
+    return fail(KGE_EINVAL, "kge_stream_batch_perm: the batch spans epochs %lld..%lld, permutations given for %lld..%lld",
+                (long long)e0, (long long)e1, (long long)epoch_lo, (long long)(epoch_lo + 1));
+  if (e1 != e0 && !perm_hi) return fail(KGE_EINVAL, "kge_stream_batch_perm: the batch straddles epochs: perm_hi needed");
+  launch_stream_gather(d->triples, d->idx_dtype == KGE_IDX_I64, d->n_rows, d->start, d->batch, perm_lo,
+                       perm_hi ? perm_hi : perm_lo, epoch_lo, d->out, (hipStream_t)stream);
+  return hip_check("kge_stream_batch_perm");
+}
+
 int32_t kge_abi_version(void) { return KGE_ABI_VERSION; }
 
 const char* kge_last_error(void) { return g_err.c_str(); }

@@ -350,6 +350,9 @@ struct RankArgs {
 kge_status launch_rank(const RankArgs& A, int mode, int proj, int sk, hipStream_t st);
 void launch_stream(const void* tri, bool i64, int64_t n, int64_t start, int64_t batch, uint64_t seed, int shuffle,
                    void* out, hipStream_t st);
+void launch_stream_perm(int64_t n, uint64_t seed, int64_t epoch, int32_t* perm, hipStream_t st);
+void launch_stream_gather(const void* tri, bool i64, int64_t n, int64_t start, int64_t batch, const int32_t* plo,
+                          const int32_t* phi, int64_t e0, void* out, hipStream_t st);
 
 __global__ void constrain_rows_kernel(float* t, int64_t rows, int32_t cols, int64_t ld, int kind,
                                       float value, StepCtl* ctl, uint32_t sig, int32_t* status);

@@ -8,7 +8,8 @@
 // repeat().batch() does). pi_e is a stateless per-epoch permutation -- a
 // 4-round Feistel network keyed by Philox4x32-10 and cycle-walked onto
 // [0, n) (include/kge_hip.h kge_stream_desc) -- so no permutation array is
-// built, stored or copied. Integer work only: one thread per output row.
+// needed; callers that stream many batches per epoch materialise pi_e once
+// (kge_stream_permutation) and gather. Integer work only: one thread per row.
 #include "kge_step.h"
 
 namespace kge {
@@ -51,10 +52,61 @@ __global__ __launch_bounds__(256) void stream_batch_kernel(const T* __restrict__
   dst[2] = src[2];
 }
 
-void launch_stream(const void* tri, bool i64, int64_t n, int64_t start, int64_t batch, uint64_t seed, int shuffle,
-                   void* out, hipStream_t st) {
+// Materialised permutations (kge_stream_permutation / kge_stream_batch_perm):
+// the cycle walk is a dependent chain of Philox rounds -- at FB15k-237 size
+// (n = 272,115 on a 2^20 domain, 26 % of values in range) the slowest of a
+// batch's 1,024 rows walks ~20 times, ~23 us per batch launch. Computed once
+// per epoch for all n positions in parallel, a batch becomes a gather.
+__global__ __launch_bounds__(256) void stream_perm_kernel(int64_t n, int h, PhiloxKey key, uint64_t epoch,
+                                                          int32_t* __restrict__ perm) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  perm[k] = (int32_t)stream_perm((uint64_t)k, (uint64_t)n, h, key, epoch);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void stream_gather_kernel(const T* __restrict__ tri, int64_t n, int64_t start,
+                                                            int64_t batch, const int32_t* __restrict__ plo,
+                                                            const int32_t* __restrict__ phi, int64_t e0,
+                                                            T* __restrict__ out) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  const int64_t p = start + b;
+  const int64_t e = p / n, k = p - e * n;
+  const int64_t row = (e == e0 ? plo : phi)[k];
+  const T* src = tri + row * 3;
+  T* dst = out + b * 3;
+  dst[0] = src[0];
+  dst[1] = src[1];
+  dst[2] = src[2];
+}
+
+static int stream_half_bits(int64_t n) {
   int w = 2;
   while (w < 64 && (1ull << w) < (uint64_t)n) w += 2;
+  return w / 2;
+}
+
+void launch_stream_perm(int64_t n, uint64_t seed, int64_t epoch, int32_t* perm, hipStream_t st) {
+  const PhiloxKey key{(uint32_t)seed, (uint32_t)(seed >> 32)};
+  hipLaunchKernelGGL(stream_perm_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n,
+                     stream_half_bits(n), key, (uint64_t)epoch, perm);
+}
+
+void launch_stream_gather(const void* tri, bool i64, int64_t n, int64_t start, int64_t batch, const int32_t* plo,
+                          const int32_t* phi, int64_t e0, void* out, hipStream_t st) {
+  const unsigned blocks = (unsigned)((batch + 255) / 256);
+  if (i64)
+    hipLaunchKernelGGL(stream_gather_kernel<int64_t>, dim3(blocks), dim3(256), 0, st, (const int64_t*)tri, n, start,
+                       batch, plo, phi, e0, (int64_t*)out);
+  else
+    hipLaunchKernelGGL(stream_gather_kernel<int32_t>, dim3(blocks), dim3(256), 0, st, (const int32_t*)tri, n, start,
+                       batch, plo, phi, e0, (int32_t*)out);
+}
+
+void launch_stream(const void* tri, bool i64, int64_t n, int64_t start, int64_t batch, uint64_t seed, int shuffle,
+                   void* out, hipStream_t st) {
+  const int w = 2 * stream_half_bits(n);
   const PhiloxKey key{(uint32_t)seed, (uint32_t)(seed >> 32)};
   const unsigned blocks = (unsigned)((batch + 255) / 256);
   if (i64)

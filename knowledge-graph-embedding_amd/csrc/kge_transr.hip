@@ -530,7 +530,12 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
     // ---- GEMM3: dM_i = X^T S[0 .. K+2) (X re-read from the table: L2); wave =
     // 16-row tile of dM with its A column in registers, column tiles in pairs
     {
-      const int nrt = (d + 15) / 16, nct = (k + 15) / 16, nkc = (NR + 15) / 16;
+      // N3: compile-time chunk count of the K + 2 slot rows (kTrKS3 / 4 at the
+      // large K the kernel is sized for: straight-line, no per-chunk branch),
+      // or 0: the runtime count
+      auto gemm3 = [&](auto n3c) {
+      constexpr int N3 = decltype(n3c)::value;
+      const int nrt = (d + 15) / 16, nct = (k + 15) / 16, nkc = N3 ? N3 : (NR + 15) / 16;
       float* dm = T.dmpart + i * (int64_t)d * k;
       // (row tile, column-tile pair) jobs in equal contiguous ranges; the A
       // column is reloaded only when the row tile changes
@@ -599,6 +604,9 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
           }
         }
       }
+      };
+      if ((NR + 15) / 16 == kTrKS3 / 4) gemm3(std::integral_constant<int, kTrKS3 / 4>{});
+      else gemm3(std::integral_constant<int, 0>{});
     }
     KGE_PROF(41);
     // ---- destination keys for the update pass

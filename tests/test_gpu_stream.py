@@ -89,3 +89,94 @@ def test_device_batcher_matches_cpu_batcher():
         g = next(gpu)
         assert g.is_cuda and g.dtype == torch.int64
         assert torch.equal(g.cpu(), next(cpu))
+
+
+def _stream_perm(data, start, batch, seed=SEED, cache=None):
+    """kge_stream_permutation + kge_stream_batch_perm (the DeviceBatcher path)."""
+    import ctypes
+    from KGE import _hip
+    L = _hip.load()
+    n = data.shape[0]
+    out = torch.full((batch, 3), -1, dtype=data.dtype, device=data.device)
+    d = _hip.kge_stream_desc()
+    d.abi_version = _hip.ABI_VERSION
+    d.idx_dtype = _hip.IDX_I64 if data.dtype == torch.int64 else _hip.IDX_I32
+    d.triples = data.data_ptr()
+    d.n_rows = n
+    d.start = start
+    d.batch = batch
+    d.seed = seed
+    d.shuffle = 1
+    d.out = out.data_ptr()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    e0, e1 = start // n, (start + batch - 1) // n
+    perms = {}
+    for e in (e0, e1):
+        perms[e] = torch.full((n,), -1, dtype=torch.int32, device=data.device)
+        _hip.check(L.kge_stream_permutation(ctypes.byref(d), e, ctypes.c_void_p(perms[e].data_ptr()), st),
+                   "kge_stream_permutation")
+    _hip.check(L.kge_stream_batch_perm(ctypes.byref(d), ctypes.c_void_p(perms[e0].data_ptr()),
+                                       ctypes.c_void_p(perms[e1].data_ptr()), e0, st), "kge_stream_batch_perm")
+    torch.cuda.synchronize()
+    return out, perms
+
+
+@pytest.mark.parametrize("dtype", [torch.int32, torch.int64])
+@pytest.mark.parametrize("n", [1, 7, 1001, 272115])
+def test_stream_perm_path_equals_per_row_walk(dtype, n):
+    """The materialised-permutation path gives kge_stream_batch's rows, bit for
+    bit, for batches inside one epoch and straddling two."""
+    data = _triples(n, dtype)
+    for start, cnt in ((0, n), (3 * n + n // 2, n), (7 * n - 1, 1), (2 * n + 1, max(1, n // 3))):
+        out, perms = _stream_perm(data, start, cnt)
+        assert torch.equal(out, _stream(data, start, cnt, 1))
+        for e, p in perms.items():   # each table is a permutation of [0, n)
+            assert torch.equal(torch.sort(p.long()).values, torch.arange(n, device="cuda"))
+
+
+def test_stream_perm_matches_oracle_small():
+    n = 64
+    data = _triples(n, torch.int64)
+    out, _ = _stream_perm(data, 5 * n + 3, 50)
+    rows = torch.tensor(O.stream_rows(n, SEED, 5 * n + 3, 50, 1), device="cuda")
+    assert torch.equal(out, data[rows])
+
+
+def test_stream_perm_rejects_bad_epochs():
+    import ctypes
+    from KGE import _hip
+    L = _hip.load()
+    n = 100
+    data = _triples(n, torch.int64)
+    out = torch.empty((60, 3), dtype=torch.int64, device="cuda")
+    perm = torch.empty(n, dtype=torch.int32, device="cuda")
+    d = _hip.kge_stream_desc()
+    d.abi_version = _hip.ABI_VERSION
+    d.idx_dtype = _hip.IDX_I64
+    d.triples = data.data_ptr()
+    d.n_rows = n
+    d.start = 70          # straddles epochs 0 and 1
+    d.batch = 60
+    d.seed = SEED
+    d.shuffle = 1
+    d.out = out.data_ptr()
+    p = ctypes.c_void_p(perm.data_ptr())
+    assert L.kge_stream_batch_perm(ctypes.byref(d), p, None, 0, None) == _hip.KGE_EINVAL     # perm_hi missing
+    assert L.kge_stream_batch_perm(ctypes.byref(d), p, p, 1, None) == _hip.KGE_EINVAL        # wrong epoch_lo
+    d.shuffle = 0
+    assert L.kge_stream_permutation(ctypes.byref(d), 0, p, None) == _hip.KGE_EINVAL
+
+
+def test_device_batcher_uses_perm_path_and_matches_host():
+    """DeviceBatcher (the train() iterator) on FB15k-237 size: three epochs of
+    batches equal the host restatement, through the materialised tables."""
+    from KGE import _philox
+    from KGE.data_utils import DeviceBatcher
+    n = 272115
+    host = (torch.arange(n * 3, dtype=torch.int64).reshape(n, 3))
+    it = DeviceBatcher(host, 100000, shuffle=True, seed=SEED, device=torch.device("cuda"), reuse_buffer=True)
+    for b in range(9):
+        out = next(it).clone()
+        rows = torch.from_numpy(_philox.stream_rows(n, SEED, b * 100000, 100000, 1)).cuda()
+        assert torch.equal(out, host.cuda()[rows])
+    assert len(it._perms) <= 2
