@@ -130,6 +130,7 @@ class KGEModel:
                     break
             else:
                 self._save_checkpoint()
+        self._join_checkpoint()
         self.sync_weights()
         self.train_loss_history = train_loss_history
         self.val_loss_history = val_loss_history
@@ -393,17 +394,53 @@ class KGEModel:
                     f.write(json.dumps({"step": step, "buckets": buckets}) + "\n")
 
     def _save_checkpoint(self):
-        """``CheckpointManager(max_to_keep=1).save()`` (``BaseModel.py:248-253``)."""
+        """``CheckpointManager(max_to_keep=1).save()`` (``BaseModel.py:248-253``).
+
+        Single device: the weights are copied into pinned host buffers on the
+        step stream (ordered before the next batch's updates) and a writer
+        thread waits for that copy and writes the file, so the next epoch's
+        batches are issued without waiting for the disk. Every reader of the
+        file (restore, the end of ``train``) joins the writer first."""
         os.makedirs(self.log_path, exist_ok=True)
         path = os.path.join(self.log_path, "ckpt.pt")
         self.sync_weights()   # multi-GPU: the shards are the authoritative entity rows (collective)
-        if _is_rank0():
-            torch.save({k: v.detach().cpu() for k, v in self.model_weights.items()}, path)
         if _world_size() > 1:
+            if _is_rank0():
+                torch.save({k: v.detach().cpu() for k, v in self.model_weights.items()}, path)
             torch.distributed.barrier()   # the file exists before any rank may restore it
+            return path
+        self._join_checkpoint()   # (its buffers are reused below)
+        on_gpu = all(v.is_cuda for v in self.model_weights.values())
+        if not on_gpu:
+            torch.save({k: v.detach().cpu() for k, v in self.model_weights.items()}, path)
+            return path
+        bufs = self.__dict__.setdefault("_ckpt_bufs", {})
+        snap = {}
+        for k, v in self.model_weights.items():
+            b = bufs.get(k)
+            if b is None or b.shape != v.shape or b.dtype != v.dtype:
+                b = bufs[k] = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+            b.copy_(v.detach(), non_blocking=True)
+            snap[k] = b
+        ev = torch.cuda.Event()
+        ev.record()
+
+        def write():
+            ev.synchronize()
+            torch.save(snap, path)
+
+        import threading
+        self._ckpt_thread = threading.Thread(target=write, daemon=True)
+        self._ckpt_thread.start()
         return path
 
+    def _join_checkpoint(self):
+        t = self.__dict__.pop("_ckpt_thread", None)
+        if t is not None:
+            t.join()
+
     def _restore_checkpoint(self):
+        self._join_checkpoint()
         path = os.path.join(self.log_path, "ckpt.pt")
         saved = torch.load(path, weights_only=True)
         with torch.no_grad():

@@ -30,7 +30,7 @@ UPDATE_PHASES = {16: "dest rows (sort+sum+apply)"}
 
 def build(extra=()):
     objs = []
-    for src in ("kge_step.hip", "kge_abi.hip", "kge_transr.hip", "kge_rel.hip", "kge_stream.hip"):
+    for src in ("kge_step.hip", "kge_abi.hip", "kge_transr.hip", "kge_rel.hip", "kge_stream.hip", "kge_exchange.hip"):
         obj = os.path.join("/tmp", "prof_" + src.replace(".hip", ".o"))
         # the bench's instance only (KGE_ONLY_ONE): seconds instead of minutes
         subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DKGE_PHASE_PROF",
