@@ -308,6 +308,10 @@ typedef struct kge_apply_desc {
  * no filter). Stream-ordered; rank_out and pos_score_out are outputs.
  */
 enum { KGE_RANK_TRANS = 0, KGE_RANK_ROT = 1, KGE_RANK_MUL = 2, KGE_RANK_DOT = 3 };
+/* KGE_RANK_FLAG_LANE_PASS: count with the lane-per-candidate pass even where
+ * the register-tiled pass applies (TRANS without a projection, MUL, DOT).
+ * Both give the same scores bit for bit, hence the same ranks (A-B / tests). */
+enum { KGE_RANK_FLAG_LANE_PASS = 1 };
 enum { KGE_RPROJ_NONE = 0, KGE_RPROJ_HYPER = 1, KGE_RPROJ_RANK1 = 2 };
 
 typedef struct kge_rank_desc {
@@ -327,7 +331,7 @@ typedef struct kge_rank_desc {
   int32_t idx_dtype;          /* KGE_IDX_* of true_ids / filt_ent               */
   int32_t score_kind;         /* KGE_SCORE_*                                    */
   float score_p;              /* 1, 2 or +inf                                   */
-  int32_t _pad;
+  int32_t flags;              /* KGE_RANK_FLAG_* (0: default)                   */
   int64_t n;                  /* queries                                        */
   const int64_t* filt_beg;    /* [n] (nullable: no filter)                      */
   const int64_t* filt_end;    /* [n]                                            */

@@ -26,6 +26,7 @@ FLAG_GRAD_RENORM = 16
 FLAG_PHASE_SCORE = 32
 FLAG_PHASE_UPDATE = 64
 RANK_TRANS, RANK_ROT, RANK_MUL, RANK_DOT = range(4)
+RANK_FLAG_LANE_PASS = 1
 RPROJ_NONE, RPROJ_HYPER, RPROJ_RANK1 = range(3)
 
 LIB_PATH = os.environ.get("KGE_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
@@ -92,7 +93,7 @@ class kge_rank_desc(ctypes.Structure):
                 ("dim", ctypes.c_int32), ("clip", ctypes.c_int32), ("q0", ctypes.c_void_p), ("q1", ctypes.c_void_p),
                 ("qw", ctypes.c_void_p), ("ldq", ctypes.c_int64), ("true_ids", ctypes.c_void_p),
                 ("idx_dtype", ctypes.c_int32), ("score_kind", ctypes.c_int32), ("score_p", ctypes.c_float),
-                ("_pad", ctypes.c_int32), ("n", ctypes.c_int64), ("filt_beg", ctypes.c_void_p),
+                ("flags", ctypes.c_int32), ("n", ctypes.c_int64), ("filt_beg", ctypes.c_void_p),
                 ("filt_end", ctypes.c_void_p), ("filt_ent", ctypes.c_void_p), ("rank_out", ctypes.c_void_p),
                 ("pos_score_out", ctypes.c_void_p), ("status", ctypes.c_void_p)]
 

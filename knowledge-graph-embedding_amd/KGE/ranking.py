@@ -242,9 +242,9 @@ def filter_index(X, positive_X, side, E):
 
 
 # ---------------------------------------------------------------- entry
-def batched_ranks(model, eval_X, corrupt_side, positive_X=None):
+def batched_ranks(model, eval_X, corrupt_side, positive_X=None, flags=0):
     """Ranks of every triple of ``eval_X`` (numpy int64 [n]), the same values
-    ``get_rank`` gives one triple at a time."""
+    ``get_rank`` gives one triple at a time. ``flags``: KGE_RANK_FLAG_*."""
     if corrupt_side not in ("h", "t"):
         raise ValueError("corrupt_side must be 'h' or 't'")
     lib = _hip.lib()
@@ -295,6 +295,7 @@ def batched_ranks(model, eval_X, corrupt_side, positive_X=None):
         d.idx_dtype = _hip.IDX_I64
         d.score_kind, d.score_p = g["score"]
         d.n = m
+        d.flags = int(flags)
         if positive_X is not None:
             gb = fb if sel is None else fb[sel].contiguous()
             ge = fe if sel is None else fe[sel].contiguous()

@@ -867,6 +867,8 @@ kge_status kge_rank(const kge_rank_desc* d, void* stream) {
   A.true_ids = d->true_ids;
   A.i64 = d->idx_dtype == KGE_IDX_I64;
   A.n = d->n;
+  if (d->flags & ~KGE_RANK_FLAG_LANE_PASS) return fail(KGE_EINVAL, "kge_rank: unknown flags 0x%x", d->flags);
+  A.lane_pass = (d->flags & KGE_RANK_FLAG_LANE_PASS) != 0;
   A.fbeg = d->filt_beg;
   A.fend = d->filt_end;
   A.fent = d->filt_ent;

@@ -226,9 +226,122 @@ __global__ __launch_bounds__(256) void rank_filter_kernel(RankArgs A) {
   if (lane_id() == 0) A.rank[q] = A.rank[q] - sub + 1ull;
 }
 
+// Register-tiled count pass for the element-wise scores (translating without
+// a projection: TransE, TransR's pre-projected candidates; DistMult; RESCAL):
+// a workgroup scores a 64-query x 64-candidate tile, each thread 4 x 4 pairs
+// held in registers, over 16-element chunks staged transposed in LDS
+// ([element][row]: a thread's four queries and four candidates are one
+// ds_read_b128 each). Candidate rows are read once per 64 queries and with
+// whole-row float4 loads (the lane-per-candidate pass reads 4 bytes of 64
+// different rows per instruction). Every pair's sum runs over the elements in
+// ascending order with the same ops as rank_scores, so the scores -- and the
+// strict > comparisons -- are bit for bit those of the pos / filter passes.
+constexpr int kRT = 64;    // queries / candidates per tile
+constexpr int kRC = 16;    // elements per staged chunk
+
+template <int MODE, int SK>
+__global__ __launch_bounds__(256) void rank_tile_kernel(RankArgs A, int64_t qt0) {
+#pragma clang fp contract(off)
+  __shared__ __attribute__((aligned(16))) float sq0[kRC][kRT];
+  __shared__ __attribute__((aligned(16))) float sq1[kRC][kRT];
+  __shared__ __attribute__((aligned(16))) float sx[kRC][kRT];
+  const int tid = threadIdx.x, tq = tid >> 4, tc = tid & 15;
+  const int64_t c0 = (int64_t)blockIdx.x * kRT, q0i = (qt0 + blockIdx.y) * kRT;
+  const bool two = (MODE == KGE_RANK_TRANS || MODE == KGE_RANK_MUL) && A.hside;   // h-side: q1 too
+  const int D = A.dim;
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  // staging: thread t loads row (t >> 2) elements 4 (t & 3) .. +3 of each tile
+  const int sr = tid >> 2, se = (tid & 3) * 4;
+  const int64_t qr = q0i + sr, er = c0 + sr;
+  const bool qv = qr < A.n, ev = er < A.E;
+  for (int e0 = 0; e0 < D; e0 += kRC) {
+    const int ne = min(kRC, D - e0);
+    float a[4], b[4], x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = e0 + se + u;
+      const bool in = se + u < ne;
+      a[u] = (qv && in) ? A.q0[qr * A.ldq + c] : 0.f;
+      b[u] = (two && qv && in) ? A.q1[qr * A.ldq + c] : 0.f;
+      x[u] = (ev && in) ? A.cand[er * A.cand_ld + c] : 0.f;
+    }
+    __syncthreads();   // the previous chunk is consumed
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sq0[se + u][sr] = a[u];
+      if (two) sq1[se + u][sr] = b[u];
+      sx[se + u][sr] = x[u];
+    }
+    __syncthreads();
+    for (int c = 0; c < ne; ++c) {
+      const float4 qa = *reinterpret_cast<const float4*>(&sq0[c][4 * tq]);
+      const float4 xa = *reinterpret_cast<const float4*>(&sx[c][4 * tc]);
+      float4 qb = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (two) qb = *reinterpret_cast<const float4*>(&sq1[c][4 * tq]);
+      const float qv0[4] = {qa.x, qa.y, qa.z, qa.w}, qv1[4] = {qb.x, qb.y, qb.z, qb.w};
+      const float xv[4] = {xa.x, xa.y, xa.z, xa.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float xe = xv[j], a0 = qv0[i];
+          if (MODE == KGE_RANK_MUL) {
+            acc[i][j] = acc[i][j] + (A.hside ? (xe * a0) * qv1[i] : a0 * xe);
+          } else if (MODE == KGE_RANK_DOT) {
+            acc[i][j] = acc[i][j] + a0 * xe;
+          } else if (SK == SK_DOT) {
+            acc[i][j] = acc[i][j] + (A.hside ? (xe + a0) * qv1[i] : a0 * xe);
+          } else {
+            const float m = fabsf(A.hside ? (xe + a0) - qv1[i] : a0 - xe);
+            if (SK == SK_P2) acc[i][j] = acc[i][j] + m * m;
+            else if (SK == SK_P1) acc[i][j] = acc[i][j] + m;
+            else if (SK == SK_PGEN) acc[i][j] = acc[i][j] + powf(m, A.p);
+            else acc[i][j] = fmaxf(acc[i][j], m);
+          }
+        }
+    }
+  }
+  // strict > the query's true score; counts summed over the 16 lanes of a row
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t q = q0i + 4 * tq + i;
+    const float pv = q < A.n ? A.pos[q] : INFINITY;
+    unsigned cnt = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float sc;
+      if (SK == SK_DOT || MODE == KGE_RANK_MUL || MODE == KGE_RANK_DOT) {
+        sc = acc[i][j];
+      } else {
+        float lpv;
+        sc = score_value<SK>(acc[i][j], A.pw, &lpv, A.p);
+      }
+      cnt += (c0 + 4 * tc + j < A.E && sc > pv) ? 1u : 0u;
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) cnt += (unsigned)__shfl_xor((int)cnt, o, KGE_WAVE);
+    if (tc == 0 && q < A.n && cnt) atomicAdd(&A.rank[q], (unsigned long long)cnt);
+  }
+}
+
 template <int MODE, int PJ, int SK>
 static void rank_launch(const RankArgs& A, hipStream_t st) {
   hipLaunchKernelGGL((rank_pos_kernel<MODE, PJ, SK>), dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, st, A);
+  if constexpr ((MODE == KGE_RANK_TRANS && PJ == KGE_RPROJ_NONE) || MODE == KGE_RANK_MUL || MODE == KGE_RANK_DOT) {
+    const int64_t nct = (A.E + kRT - 1) / kRT, nqt = (A.n + kRT - 1) / kRT;
+    constexpr int64_t kMaxY = 65535;
+    if (!A.lane_pass && nct <= ((int64_t)1 << 31) - 1) {
+      for (int64_t t0 = 0; t0 < nqt; t0 += kMaxY)
+        hipLaunchKernelGGL((rank_tile_kernel<MODE, SK>), dim3((unsigned)nct, (unsigned)std::min(nqt - t0, kMaxY)),
+                           dim3(256), 0, st, A, t0);
+      hipLaunchKernelGGL((rank_filter_kernel<MODE, PJ, SK>), dim3((unsigned)((A.n + 3) / 4)), dim3(256), 0, st, A);
+      return;
+    }
+  }
   const int64_t nchunk = (A.E + kRankThreads - 1) / kRankThreads;
   const int64_t ng = (A.n + kRankQ - 1) / kRankQ;
   const size_t lds = (size_t)3 * kRankQ * ((A.dim + 3) & ~3) * 4;

@@ -338,6 +338,7 @@ struct RankArgs {
   bool clip;                              // TransD: projected rows clipped to norm <= 1
   bool hside;                             // corrupt_side 'h'
   bool pw;                                // LpDistancePow
+  bool lane_pass;                         // KGE_RANK_FLAG_LANE_PASS
   float p;                                // LpDistance p (SK_PGEN)
   const float* q0; const float* q1; const float* qw; int64_t ldq;
   const void* true_ids; bool i64; int64_t n;

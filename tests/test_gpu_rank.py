@@ -118,3 +118,35 @@ def test_rank_fb15k237_slice_transe_d200():
         ref, ties = _per_triple(m, X, side, T)
         _check(got, ref, ties)
         assert (got > 1).any()
+
+
+@pytest.mark.parametrize("name,si", [("TransE", 0), ("TransE", 1), ("TransE", 2), ("TransE", 3), ("TransE", 4),
+                                     ("TransE", 5), ("DistMult", None), ("RESCAL", None), ("TransR", 0)])
+def test_rank_tiled_pass_equals_lane_pass(name, si):
+    """The register-tiled count pass and the lane-per-candidate pass score with
+    the same ops in the same order: identical ranks, integer for integer, on a
+    FB15k-237-sized candidate set (E = 14,541) with 333 queries per side,
+    filtered by the whole training set -- including ranks decided by ties."""
+    from KGE import _hip, ranking, score
+    from tests.test_plugin_surface import build
+    z = np.load(os.path.join(ROOT, "data", "fb15k237_train.npz"))
+    T = z["triples"].astype(np.int64)
+    E, R = int(z["n_entities"]), int(z["n_relations"])
+    sc = None if si is None else [score.LpDistance(2), score.LpDistance(1), score.LpDistance(np.inf),
+                                  score.LpDistancePow(2), score.Dot(), score.LpDistance(3)][si]
+    m = build(name, sc)
+    m.metadata = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
+    m._model_weights_initial = None
+    m._init_embeddings(seed=5)
+    m._to_device()
+    X = T[np.random.default_rng(2).choice(len(T), 333, replace=False)]
+    # a few duplicated candidate rows: exact ties with the true entity's score
+    with torch.no_grad():
+        w = m.model_weights["ent_emb"]
+        w[(X[:20, 0] + 1) % E] = w[X[:20, 0]]
+        w[(X[:20, 2] + 1) % E] = w[X[:20, 2]]
+    PX = torch.as_tensor(T, device=w.device)
+    for side in ("h", "t"):
+        tiled = ranking.batched_ranks(m, X, side, PX)
+        lane = ranking.batched_ranks(m, X, side, PX, flags=_hip.RANK_FLAG_LANE_PASS)
+        assert np.array_equal(tiled, lane), np.nonzero(tiled != lane)[0][:10]
