@@ -239,21 +239,22 @@ __global__ __launch_bounds__(256) void rank_filter_kernel(RankArgs A) {
 constexpr int kRT = 64;    // queries / candidates per tile
 constexpr int kRC = 16;    // elements per staged chunk
 
-template <int MODE, int SK>
+template <int MODE, int SK, bool HS>
 __global__ __launch_bounds__(256) void rank_tile_kernel(RankArgs A, int64_t qt0) {
 #pragma clang fp contract(off)
+  using f2 = __attribute__((ext_vector_type(2))) float;
   __shared__ __attribute__((aligned(16))) float sq0[kRC][kRT];
   __shared__ __attribute__((aligned(16))) float sq1[kRC][kRT];
   __shared__ __attribute__((aligned(16))) float sx[kRC][kRT];
   const int tid = threadIdx.x, tq = tid >> 4, tc = tid & 15;
   const int64_t c0 = (int64_t)blockIdx.x * kRT, q0i = (qt0 + blockIdx.y) * kRT;
-  const bool two = (MODE == KGE_RANK_TRANS || MODE == KGE_RANK_MUL) && A.hside;   // h-side: q1 too
+  constexpr bool two = (MODE == KGE_RANK_TRANS || MODE == KGE_RANK_MUL) && HS;   // h-side: q1 too
   const int D = A.dim;
-  float acc[4][4];
+  // pairs (i, 2jp) and (i, 2jp + 1) side by side: the element ops run as
+  // packed f32 (v_pk_add / v_pk_mul), each lane of a pair in the scalar order
+  f2 acc[4][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f2{0.f, 0.f};
   // staging: thread t loads row (t >> 2) elements 4 (t & 3) .. +3 of each tile
   const int sr = tid >> 2, se = (tid & 3) * 4;
   const int64_t qr = q0i + sr, er = c0 + sr;
@@ -283,26 +284,36 @@ __global__ __launch_bounds__(256) void rank_tile_kernel(RankArgs A, int64_t qt0)
       float4 qb = make_float4(0.f, 0.f, 0.f, 0.f);
       if (two) qb = *reinterpret_cast<const float4*>(&sq1[c][4 * tq]);
       const float qv0[4] = {qa.x, qa.y, qa.z, qa.w}, qv1[4] = {qb.x, qb.y, qb.z, qb.w};
-      const float xv[4] = {xa.x, xa.y, xa.z, xa.w};
+      const f2 xp[2] = {f2{xa.x, xa.y}, f2{xa.z, xa.w}};
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
+        const f2 a0 = f2{qv0[i], qv0[i]}, a1 = f2{qv1[i], qv1[i]};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float xe = xv[j], a0 = qv0[i];
+        for (int jp = 0; jp < 2; ++jp) {
+          const f2 xe = xp[jp];
+          f2& ac = acc[i][jp];
           if (MODE == KGE_RANK_MUL) {
-            acc[i][j] = acc[i][j] + (A.hside ? (xe * a0) * qv1[i] : a0 * xe);
+            ac = ac + (HS ? (xe * a0) * a1 : a0 * xe);
           } else if (MODE == KGE_RANK_DOT) {
-            acc[i][j] = acc[i][j] + a0 * xe;
+            ac = ac + a0 * xe;
           } else if (SK == SK_DOT) {
-            acc[i][j] = acc[i][j] + (A.hside ? (xe + a0) * qv1[i] : a0 * xe);
+            ac = ac + (HS ? (xe + a0) * a1 : a0 * xe);
           } else {
-            const float m = fabsf(A.hside ? (xe + a0) - qv1[i] : a0 - xe);
-            if (SK == SK_P2) acc[i][j] = acc[i][j] + m * m;
-            else if (SK == SK_P1) acc[i][j] = acc[i][j] + m;
-            else if (SK == SK_PGEN) acc[i][j] = acc[i][j] + powf(m, A.p);
-            else acc[i][j] = fmaxf(acc[i][j], m);
+            const f2 d = HS ? (xe + a0) - a1 : a0 - xe;
+            if (SK == SK_P2) {
+              ac = ac + d * d;   // |d| |d| == d d bit for bit
+            } else {
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const float m = fabsf(d[h]);
+                if (SK == SK_P1) ac[h] = ac[h] + m;
+                else if (SK == SK_PGEN) ac[h] = ac[h] + powf(m, A.p);
+                else ac[h] = fmaxf(ac[h], m);
+              }
+            }
           }
         }
+      }
     }
   }
   // strict > the query's true score; counts summed over the 16 lanes of a row
@@ -313,12 +324,13 @@ __global__ __launch_bounds__(256) void rank_tile_kernel(RankArgs A, int64_t qt0)
     unsigned cnt = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
+      const float av = acc[i][j >> 1][j & 1];
       float sc;
       if (SK == SK_DOT || MODE == KGE_RANK_MUL || MODE == KGE_RANK_DOT) {
-        sc = acc[i][j];
+        sc = av;
       } else {
         float lpv;
-        sc = score_value<SK>(acc[i][j], A.pw, &lpv, A.p);
+        sc = score_value<SK>(av, A.pw, &lpv, A.p);
       }
       cnt += (c0 + 4 * tc + j < A.E && sc > pv) ? 1u : 0u;
     }
@@ -328,6 +340,84 @@ __global__ __launch_bounds__(256) void rank_tile_kernel(RankArgs A, int64_t qt0)
   }
 }
 
+// Filter pass for the tiled modes: wave per query, 64 filtered entities per
+// round, one per lane. Their rows are staged through the wave's LDS 16
+// elements at a time (float4 loads along each row, written transposed) so a
+// lane sums its entity's elements in ascending order from LDS -- the same ops
+// and order as rank_scores, hence exactly the scores the count pass compared
+// -- without 64 scattered row reads per element.
+template <int MODE, int SK>
+__global__ __launch_bounds__(256) void rank_filter_tile_kernel(RankArgs A) {
+#pragma clang fp contract(off)
+  __shared__ __attribute__((aligned(16))) float sx[4][kRC][KGE_WAVE];
+  const int lane = lane_id(), wv = wave_id();
+  const int64_t q = (int64_t)blockIdx.x * 4 + wv;
+  if (q >= A.n) return;
+  unsigned long long sub = 0;
+  if (A.fbeg) {
+    const float pv = A.pos[q];
+    const float* r0 = A.q0 + q * A.ldq;
+    const float* r1 = (A.q1 && A.hside) ? A.q1 + q * A.ldq : nullptr;
+    const int D = A.dim;
+    float (*T)[KGE_WAVE] = sx[wv];
+    for (int64_t j0 = A.fbeg[q]; j0 < A.fend[q]; j0 += KGE_WAVE) {
+      const int cnt = (int)min<int64_t>(KGE_WAVE, A.fend[q] - j0);
+      int64_t e = 0;
+      bool ok = lane < cnt;
+      if (ok) {
+        e = load_idx(A.fent, j0 + lane, A.i64);
+        if (e < 0 || e >= A.E) { set_status(A.status, KGE_ERANGE); ok = false; e = 0; }
+      }
+      float acc = 0.f;
+      for (int e0 = 0; e0 < D; e0 += kRC) {
+        const int ne = min(kRC, D - e0);
+        // staging: 64 rows x 16 elements, four (row, element quad) per lane
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int idx = k * KGE_WAVE + lane, r = idx >> 2, u0 = (idx & 3) * 4;
+          const int64_t er = __shfl(e, r, KGE_WAVE);
+          const bool rv = r < cnt;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+            T[u0 + u][r] = (rv && u0 + u < ne) ? A.cand[er * A.cand_ld + e0 + u0 + u] : 0.f;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int c = 0; c < ne; ++c) {
+          const float xe = T[c][lane], a0 = r0[e0 + c];
+          if (MODE == KGE_RANK_MUL) {
+            acc = acc + (A.hside ? (xe * a0) * r1[e0 + c] : a0 * xe);
+          } else if (MODE == KGE_RANK_DOT) {
+            acc = acc + a0 * xe;
+          } else if (SK == SK_DOT) {
+            acc = acc + (A.hside ? (xe + a0) * r1[e0 + c] : a0 * xe);
+          } else {
+            const float m = fabsf(A.hside ? (xe + a0) - r1[e0 + c] : a0 - xe);
+            if (SK == SK_P2) acc = acc + m * m;
+            else if (SK == SK_P1) acc = acc + m;
+            else if (SK == SK_PGEN) acc = acc + powf(m, A.p);
+            else acc = fmaxf(acc, m);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      float sc;
+      if (SK == SK_DOT || MODE == KGE_RANK_MUL || MODE == KGE_RANK_DOT) {
+        sc = acc;
+      } else {
+        float lpv;
+        sc = score_value<SK>(acc, A.pw, &lpv, A.p);
+      }
+      sub += (ok && sc > pv) ? 1ull : 0ull;
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) sub += __shfl_xor(sub, o, KGE_WAVE);
+  if (lane == 0) A.rank[q] = A.rank[q] - sub + 1ull;
+}
+
 template <int MODE, int PJ, int SK>
 static void rank_launch(const RankArgs& A, hipStream_t st) {
   hipLaunchKernelGGL((rank_pos_kernel<MODE, PJ, SK>), dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, st, A);
@@ -335,10 +425,12 @@ static void rank_launch(const RankArgs& A, hipStream_t st) {
     const int64_t nct = (A.E + kRT - 1) / kRT, nqt = (A.n + kRT - 1) / kRT;
     constexpr int64_t kMaxY = 65535;
     if (!A.lane_pass && nct <= ((int64_t)1 << 31) - 1) {
-      for (int64_t t0 = 0; t0 < nqt; t0 += kMaxY)
-        hipLaunchKernelGGL((rank_tile_kernel<MODE, SK>), dim3((unsigned)nct, (unsigned)std::min(nqt - t0, kMaxY)),
-                           dim3(256), 0, st, A, t0);
-      hipLaunchKernelGGL((rank_filter_kernel<MODE, PJ, SK>), dim3((unsigned)((A.n + 3) / 4)), dim3(256), 0, st, A);
+      for (int64_t t0 = 0; t0 < nqt; t0 += kMaxY) {
+        const dim3 grid((unsigned)nct, (unsigned)std::min(nqt - t0, kMaxY));
+        if (A.hside) hipLaunchKernelGGL((rank_tile_kernel<MODE, SK, true>), grid, dim3(256), 0, st, A, t0);
+        else hipLaunchKernelGGL((rank_tile_kernel<MODE, SK, false>), grid, dim3(256), 0, st, A, t0);
+      }
+      hipLaunchKernelGGL((rank_filter_tile_kernel<MODE, SK>), dim3((unsigned)((A.n + 3) / 4)), dim3(256), 0, st, A);
       return;
     }
   }
