@@ -352,66 +352,108 @@ __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T
     float rsum[kTrKV];
 #pragma unroll
     for (int v = 0; v < kTrKV; ++v) rsum[v] = 0.f;
+    // Three passes over the wave's slots so the per-slot wave sums go through
+    // two batched transposed reductions (multi_reduce: the same tree as wsum,
+    // so the same bits) instead of five sequential reductions per slot.
+    static_assert(3 * kTrQ <= 32, "batched slot reductions hold 32 values");
+    float red[32];
+#pragma unroll
+    for (int t = 0; t < 32; ++t) red[t] = 0.f;
+    // pass A: raw slice gradients (G[m][0] x side, G[m][1] y side), x . g_x, y . g_y
 #pragma unroll
     for (int m = 0; m < kTrQ; ++m) {
       const int q = wv + kTrWaves * m;
-      if (q > K) break;
-      const int kind = kind_of(q);
-      const int xr = xrow_of(q, kind), yr = yrow_of(q, kind);
-      const float* xp = P + xr * LP;
-      const float* yp = P + yr * LP;
-      const float alpha = sA[q], Mx = SK == SK_PGEN ? A.p : sR[q];
-      float gx[kTrKV], gy[kTrKV];
-      float gxx = 0.f, dx = 0.f, dy = 0.f;
 #pragma unroll
-      for (int v = 0; v < kTrKV; ++v) {
-        const int c = lane + KGE_WAVE * v;
-        gx[v] = gy[v] = 0.f;
-        if (c < k) {
-          const float x = xp[c] + rr[v], y = yp[c];
-          if (SK == SK_DOT) {
-            gx[v] = alpha * y;
-            gy[v] = alpha * x;
-          } else {
-            gx[v] = lp_elem_grad<SK>(x - y, alpha, Mx);
-            gy[v] = -gx[v];
+      for (int v = 0; v < kTrKV; ++v) G[m][0][v] = G[m][1][v] = 0.f;
+      if (q <= K) {
+        const int kind = kind_of(q);
+        const float* xp = P + xrow_of(q, kind) * LP;
+        const float* yp = P + yrow_of(q, kind) * LP;
+        const float alpha = sA[q], Mx = SK == SK_PGEN ? A.p : sR[q];
+        float gxx = 0.f, dx = 0.f, dy = 0.f;
+#pragma unroll
+        for (int v = 0; v < kTrKV; ++v) {
+          const int c = lane + KGE_WAVE * v;
+          if (c < k) {
+            const float x = xp[c] + rr[v], y = yp[c];
+            float gx, gy;
+            if (SK == SK_DOT) {
+              gx = alpha * y;
+              gy = alpha * x;
+            } else {
+              gx = lp_elem_grad<SK>(x - y, alpha, Mx);
+              gy = -gx;
+            }
+            gxx += gx * gx;
+            rsum[v] += gx;               // the r-lookup slice is d s / d x
+            dx += gx * xp[c];
+            dy += gy * yp[c];
+            G[m][0][v] = gx;
+            G[m][1][v] = gy;
           }
-          gxx += gx[v] * gx[v];
-          rsum[v] += gx[v];               // the r-lookup slice is d s / d x
-          dx += gx[v] * xp[c];
-          dy += gy[v] * yp[c];
         }
+        n_rel += gxx;
+        red[2 * m] = dx;
+        red[2 * m + 1] = dy;
       }
-      n_rel += gxx;
-      dx = wsum(dx);
-      dy = wsum(dy);
-      // through clip_constraint: rows with norm >= 1 were divided by it
-      const float nx = pn[xr], ny = pn[yr];
-      const bool cx = T.clip && !(nx < 1.f), cy = T.clip && !(ny < 1.f);
-      float a2 = 0.f, b2 = 0.f, ab = 0.f;
+    }
+    const float dxy = multi_reduce<32, false>(red);   // lane l: value l >> 1
+    auto bcast = [](float v, int src) {
+      return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src));
+    };
+    // pass B: back through clip_constraint (rows with norm >= 1 were divided by it)
 #pragma unroll
-      for (int v = 0; v < kTrKV; ++v) {
-        const int c = lane + KGE_WAVE * v;
-        if (c < k) {
-          if (cx) gx[v] = (gx[v] - dx * xp[c]) / nx;
-          if (cy) gy[v] = (gy[v] - dy * yp[c]) / ny;
+    for (int t = 0; t < 32; ++t) red[t] = 0.f;
+#pragma unroll
+    for (int m = 0; m < kTrQ; ++m) {
+      const int q = wv + kTrWaves * m;
+      if (q <= K) {
+        const int kind = kind_of(q);
+        const int xr = xrow_of(q, kind), yr = yrow_of(q, kind);
+        const float* xp = P + xr * LP;
+        const float* yp = P + yr * LP;
+        const float dx = bcast(dxy, (2 * m) << 1), dy = bcast(dxy, (2 * m + 1) << 1);
+        const float nx = pn[xr], ny = pn[yr];
+        const bool cx = T.clip && !(nx < 1.f), cy = T.clip && !(ny < 1.f);
+        float a2 = 0.f, b2 = 0.f, ab = 0.f;
+#pragma unroll
+        for (int v = 0; v < kTrKV; ++v) {
+          const int c = lane + KGE_WAVE * v;
+          if (c < k) {
+            if (cx) G[m][0][v] = (G[m][0][v] - dx * xp[c]) / nx;
+            if (cy) G[m][1][v] = (G[m][1][v] - dy * yp[c]) / ny;
+          }
+          a2 += G[m][0][v] * G[m][0][v];
+          b2 += G[m][1][v] * G[m][1][v];
+          ab += G[m][0][v] * G[m][1][v];
         }
-        a2 += gx[v] * gx[v];
-        b2 += gy[v] * gy[v];
-        ab += gx[v] * gy[v];
+        red[3 * m] = a2;
+        red[3 * m + 1] = b2;
+        red[3 * m + 2] = ab;
       }
-      a2 = wsum(a2);
-      b2 = wsum(b2);
-      ab = wsum(ab);
-      // rel_proj slice of this triple: x_h (x) g_h + x_t (x) g_t
-      const float hx = xx[xr], tx = xx[yr];
-      const float htx = kind == KIND_POS ? xh[1] : (kind == KIND_TC ? xh[2 + q] : xt[2 + q]);
-      n_proj += hx * a2 + tx * b2 + 2.f * htx * ab;
-      // x side is the head's projection, y side the tail's
+    }
+    const float abr = multi_reduce<32, false>(red);
+    // pass C: the rel_proj slice norms (x_h (x) g_h + x_t (x) g_t); the x side
+    // is the head's projection, the y side the tail's
 #pragma unroll
-      for (int v = 0; v < kTrKV; ++v) {
-        if (kind == KIND_HC) { G[m][0][v] = gy[v]; G[m][1][v] = gx[v]; }
-        else { G[m][0][v] = gx[v]; G[m][1][v] = gy[v]; }
+    for (int m = 0; m < kTrQ; ++m) {
+      const int q = wv + kTrWaves * m;
+      if (q <= K) {
+        const int kind = kind_of(q);
+        const int xr = xrow_of(q, kind), yr = yrow_of(q, kind);
+        const float a2 = bcast(abr, (3 * m) << 1), b2 = bcast(abr, (3 * m + 1) << 1),
+                    ab = bcast(abr, (3 * m + 2) << 1);
+        const float hx = xx[xr], tx = xx[yr];
+        const float htx = kind == KIND_POS ? xh[1] : (kind == KIND_TC ? xh[2 + q] : xt[2 + q]);
+        n_proj += hx * a2 + tx * b2 + 2.f * htx * ab;
+        if (kind == KIND_HC) {
+#pragma unroll
+          for (int v = 0; v < kTrKV; ++v) {
+            const float t = G[m][0][v];
+            G[m][0][v] = G[m][1][v];
+            G[m][1][v] = t;
+          }
+        }
       }
     }
     __syncthreads();   // P is dead from here: S overwrites X and P

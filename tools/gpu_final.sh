@@ -29,4 +29,6 @@ for a in "--force-exchange" "--force-exchange --loopback"; do
 done
 timeout -k 10 300 python -u bench.py --workload c2 --force-exchange --no-cpu-baseline > "$OUT/bench_c2_fx.json" 2> "$OUT/bench_c2_fx.err" || { tail -20 "$OUT/bench_c2_fx.err"; exit 9; }
 cat "$OUT/bench_c2_fx.json"
+timeout -k 10 200 python -u tools/transr_prof.py run > "$OUT/transr_phases.txt" 2>&1 || { tail -20 "$OUT/transr_phases.txt"; exit 10; }
+grep -v amdgpu.ids "$OUT/transr_phases.txt"
 echo FINAL_OK
