@@ -340,8 +340,9 @@ __global__ __launch_bounds__(256) void rank_tile_kernel(RankArgs A, int64_t qt0)
   }
 }
 
-// Filter pass for the tiled modes: wave per query, 64 filtered entities per
-// round, one per lane. Their rows are staged through the wave's LDS 16
+// Filter pass for the tiled modes: workgroup per query, its four waves take
+// turns at 64 filtered entities per round, one per lane (a long filter list
+// -- thousands of known heads of one (r, t) -- is spread over four waves). Their rows are staged through the wave's LDS 16
 // elements at a time (float4 loads along each row, written transposed) so a
 // lane sums its entity's elements in ascending order from LDS -- the same ops
 // and order as rank_scores, hence exactly the scores the count pass compared
@@ -350,9 +351,9 @@ template <int MODE, int SK>
 __global__ __launch_bounds__(256) void rank_filter_tile_kernel(RankArgs A) {
 #pragma clang fp contract(off)
   __shared__ __attribute__((aligned(16))) float sx[4][kRC][KGE_WAVE];
+  __shared__ unsigned long long s_sub[4];
   const int lane = lane_id(), wv = wave_id();
-  const int64_t q = (int64_t)blockIdx.x * 4 + wv;
-  if (q >= A.n) return;
+  const int64_t q = blockIdx.x;
   unsigned long long sub = 0;
   if (A.fbeg) {
     const float pv = A.pos[q];
@@ -360,7 +361,7 @@ __global__ __launch_bounds__(256) void rank_filter_tile_kernel(RankArgs A) {
     const float* r1 = (A.q1 && A.hside) ? A.q1 + q * A.ldq : nullptr;
     const int D = A.dim;
     float (*T)[KGE_WAVE] = sx[wv];
-    for (int64_t j0 = A.fbeg[q]; j0 < A.fend[q]; j0 += KGE_WAVE) {
+    for (int64_t j0 = A.fbeg[q] + wv * KGE_WAVE; j0 < A.fend[q]; j0 += 4 * KGE_WAVE) {
       const int cnt = (int)min<int64_t>(KGE_WAVE, A.fend[q] - j0);
       int64_t e = 0;
       bool ok = lane < cnt;
@@ -415,7 +416,9 @@ __global__ __launch_bounds__(256) void rank_filter_tile_kernel(RankArgs A) {
     }
   }
   for (int o = 32; o >= 1; o >>= 1) sub += __shfl_xor(sub, o, KGE_WAVE);
-  if (lane == 0) A.rank[q] = A.rank[q] - sub + 1ull;
+  if (lane == 0) s_sub[wv] = sub;
+  __syncthreads();
+  if (threadIdx.x == 0) A.rank[q] = A.rank[q] - (s_sub[0] + s_sub[1] + s_sub[2] + s_sub[3]) + 1ull;
 }
 
 template <int MODE, int PJ, int SK>
@@ -430,7 +433,7 @@ static void rank_launch(const RankArgs& A, hipStream_t st) {
         if (A.hside) hipLaunchKernelGGL((rank_tile_kernel<MODE, SK, true>), grid, dim3(256), 0, st, A, t0);
         else hipLaunchKernelGGL((rank_tile_kernel<MODE, SK, false>), grid, dim3(256), 0, st, A, t0);
       }
-      hipLaunchKernelGGL((rank_filter_tile_kernel<MODE, SK>), dim3((unsigned)((A.n + 3) / 4)), dim3(256), 0, st, A);
+      hipLaunchKernelGGL((rank_filter_tile_kernel<MODE, SK>), dim3((unsigned)A.n), dim3(256), 0, st, A);
       return;
     }
   }
