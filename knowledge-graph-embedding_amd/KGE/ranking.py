@@ -224,17 +224,22 @@ def filter_index(X, positive_X, side, E):
     P = positive_X.to(torch.int64)
     key = P[:, 1] * E + P[:, keep]            # < R * E: fits int64 for any table
     ent = P[:, corrupt]
-    # (key, entity) pairs sorted lexicographically by two stable sorts (a
-    # combined key * E + entity overflows int64 once R * E^2 > 2^63), then
-    # de-duplicated
-    o = torch.argsort(ent, stable=True)
-    key, ent = key[o], ent[o]
-    o = torch.argsort(key, stable=True)
-    key, ent = key[o], ent[o]
-    first = torch.ones_like(key, dtype=torch.bool)
-    if key.numel() > 1:
-        first[1:] = (key[1:] != key[:-1]) | (ent[1:] != ent[:-1])
-    keys, ents = key[first], ent[first]
+    # (key, entity) pairs sorted lexicographically, then de-duplicated: one
+    # sort of the combined key * E + entity while it fits int64, two stable
+    # sorts once R * E^2 > 2^63
+    R = int(P[:, 1].max().item()) + 1 if P.numel() else 1
+    if R * E * E < (1 << 62):
+        u = torch.unique(key * E + ent)   # sorted, unique
+        keys, ents = u // E, u % E
+    else:
+        o = torch.argsort(ent, stable=True)
+        key, ent = key[o], ent[o]
+        o = torch.argsort(key, stable=True)
+        key, ent = key[o], ent[o]
+        first = torch.ones_like(key, dtype=torch.bool)
+        if key.numel() > 1:
+            first[1:] = (key[1:] != key[:-1]) | (ent[1:] != ent[:-1])
+        keys, ents = key[first], ent[first]
     qk = X[:, 1].to(torch.int64) * E + X[:, keep].to(torch.int64)
     beg = torch.searchsorted(keys, qk, right=False)
     end = torch.searchsorted(keys, qk, right=True)
