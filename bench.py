@@ -228,7 +228,10 @@ def accounting(w, B, K, d, E, R, batch):
     if m == "TransE":
         step, score, upd, con = transe_bytes(B, K, d, E)
         rows, context = transe_update_bytes(B, K, d, E, batch, w["constraint"])
-        return {"bound": "hbm", "step": step, "kernels": {"score_kernel": score, "update_kernel": rows + context},
+        # update_kernel against HBM: the rows it rewrites; its per-key context
+        # rows / coefficients / list entries (L2-resident, written by the score
+        # kernel just before) are reported beside it, not counted as HBM bytes
+        return {"bound": "hbm", "step": step, "kernels": {"score_kernel": score, "update_kernel": rows},
                 "update_split": {"rows_bytes": rows, "context_bytes": context}}
     if m == "RotatE":
         # entity rows 2d floats (8d bytes), relation rows d phases (4d bytes)
@@ -239,8 +242,11 @@ def accounting(w, B, K, d, E, R, batch):
         ur = int(torch.unique(batch[:, 1]).numel())
         sparse = 2 * (4 * d * (2 * B + B * K) + 4 * d * d * ur)
         dense = 2 * 4 * (E * d + R * d * d)
+        # score_kernel: the positives' rows, one row per negative, the ids,
+        # and every live relation's R_r once (the in-kernel context / post
+        # products u = R^T h, v = R t, R A, R^T B; repeats are cache hits)
         return {"bound": "hbm", "step": sparse + dense, "distinct_relations": ur,
-                "kernels": {"score_kernel": 4 * d * (3 * B + B * K) + 12 * B}}
+                "kernels": {"score_kernel": 4 * d * (3 * B + B * K) + 12 * B + 4 * d * d * ur}}
     # TransR: three products per positive: P = X M (K+2 rows), S M^T (2K+4
     # slice rows: every slice's ||M g||^2 is a clip_by_norm term), X^T S' (K+2)
     flops = 2.0 * d * d * (4 * K + 8) * B
@@ -297,6 +303,7 @@ def hbm_point(args, dev, R):
     pmc = pmc_traffic("c2-50m")
     out["traffic"] = pmc["kernels"][dom].get("hbm_bytes_per_launch") \
         if pmc and dom in pmc.get("kernels", {}) else None
+    out["traffic_source"] = pmc["_source"] if out["traffic"] is not None else None
     del step, model, batches
     torch.cuda.empty_cache()
     return out
@@ -314,13 +321,31 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def host_cores():
+    """Every core this process may run on (``nproc``: the affinity mask; SURVEY
+    8(d): torch.set_num_threads over all of them). The box's OMP_NUM_THREADS
+    is recorded beside it, not obeyed."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cgroup_cpu_max():
+    """The cgroup v2 CPU quota ("max 100000" = unlimited), if readable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
 def cpu_baseline(triples, E, R, B, K, d, budget_s):
     """Time the CPU restatement (oracle, fp32 torch autograd on the host) on a
     bounded sample: whole C2 steps until ~budget_s seconds of CPU work, with
     every core, then a shorter single-thread sample."""
     from oracle import kge_oracle as orc
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
-    threads = min(threads, os.cpu_count() or threads)
+    threads = host_cores()
     rng = np.random.default_rng(0)
 
     def run(nthreads, budget):
@@ -343,7 +368,9 @@ def cpu_baseline(triples, E, R, B, K, d, budget_s):
     n1, t1 = run(1, max(budget_s / 3, 3.0))
     torch.set_num_threads(threads)
     return {"value": n * B / t, "unit": "positive-triples/s", "cores": threads, "kind": "port",
-            "single_thread_value": n1 * B / t1, "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+            "single_thread_value": n1 * B / t1, "cpu_model": cpu_model(), "nproc": threads,
+            "cpu_count": os.cpu_count(), "env_omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "cgroup_cpu_max": cgroup_cpu_max(),
             "sample": "%d whole C2 steps (B=%d, K=%d, d=%d, FB15k-237) of the fp32 torch-CPU restatement "
                       "(oracle/kge_oracle.py) on %d threads, %.1f s; single thread: %d steps, %.1f s"
                       % (n, B, K, d, threads, t, n1, t1)}
@@ -351,11 +378,15 @@ def cpu_baseline(triples, E, R, B, K, d, budget_s):
 
 def pmc_traffic(workload):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    --pmc summary (tools/pmc_traffic.py), or None."""
+    --pmc summary (tools/pmc_traffic.py), or None. NOT measured in this run:
+    the counters need their own rocprofv3 --pmc pass; the line names the file
+    (``traffic_source``)."""
     name = "pmc_traffic.json" if workload == "c2" else "pmc_traffic_%s.json" % workload
     try:
         with open(os.path.join(ROOT, "profiles", name)) as f:
-            return json.load(f)
+            out = json.load(f)
+        out["_source"] = "profiles/%s (rocprofv3 --pmc, committed; not this run)" % name
+        return out
     except (OSError, ValueError):
         return None
 
@@ -491,7 +522,7 @@ def eval_leg(args, dev):
                     ns_strategy=UniformStrategy(np.arange(E), seed=1), constraint=w["constraint"])
         cm.metadata = model.metadata
         cm.model_weights = {k: v.detach().cpu() for k, v in model.model_weights.items()}
-        threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1, os.cpu_count() or 1)
+        threads = host_cores()
         torch.set_num_threads(threads)
         k, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < min(args.cpu_seconds, 10.0):
@@ -629,7 +660,7 @@ def main():
     if acc["bound"] == "hbm":
         kern = {k: {"ms": round(group_ms[k], 5), "GBps": round(acc["kernels"][k] / (group_ms[k] * 1e-3) / 1e9, 1)}
                 for k in group_ms}
-        dom = names[0]
+        dom = max(group_ms, key=group_ms.get)   # the longer launch (group) of the step
         ach = acc["kernels"][dom] / (group_ms[dom] * 1e-3) / 1e9
         pmc = pmc_traffic(args.workload)
         traffic = None
@@ -637,6 +668,7 @@ def main():
             traffic = pmc["kernels"][dom].get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_source": pmc["_source"] if traffic is not None else None,
                 "step": {"alg_bytes": acc["step"], "ms_per_step": round(ms, 5),
                          "achieved": round(acc["step"] / (ms * 1e-3) / 1e9, 1),
                          "frac": round(acc["step"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},

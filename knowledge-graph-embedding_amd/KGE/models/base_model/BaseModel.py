@@ -97,6 +97,21 @@ class KGEModel:
         self.best_step = None
 
         logging.info("[%s] Start Training..." % str(datetime.datetime.now()))
+        try:
+            self._train_epochs(epochs, train_iter, val_iter, early_stopping_rounds, restore_best_weight,
+                               train_loss_history, val_loss_history, patience_count)
+        finally:
+            self._join_checkpoint()   # (also when an epoch raised: no writer outlives train())
+        self.sync_weights()
+        self.train_loss_history = train_loss_history
+        self.val_loss_history = val_loss_history
+        if log_projector:
+            self._log_embeddings_projector(log_path)
+        logging.info("[%s] Finished training!" % str(datetime.datetime.now()))
+
+    def _train_epochs(self, epochs, train_iter, val_iter, early_stopping_rounds, restore_best_weight,
+                      train_loss_history, val_loss_history, patience_count):
+        """The epoch loop of ``BaseModel.py:100-184``."""
         for i in range(epochs):
             # per-epoch loss sums stay on the device: the fused step adds each
             # batch's loss into them itself (no per-batch host work); the host
@@ -121,7 +136,7 @@ class KGEModel:
             self._log_embeddings_histogram(i)
 
             if early_stopping_rounds is not None:
-                assert val_X is not None, "val_X should be given if want to check early stopping."
+                assert val_iter is not None, "val_X should be given if want to check early stopping."
                 early_stop, patience_count = self._check_early_stopping(
                     val_loss_history, "larger", patience_count, early_stopping_rounds, i, restore_best_weight)
                 if early_stop:
@@ -130,13 +145,6 @@ class KGEModel:
                     break
             else:
                 self._save_checkpoint()
-        self._join_checkpoint()
-        self.sync_weights()
-        self.train_loss_history = train_loss_history
-        self.val_loss_history = val_loss_history
-        if log_projector:
-            self._log_embeddings_projector(log_path)
-        logging.info("[%s] Finished training!" % str(datetime.datetime.now()))
 
     def _prepare_for_train(self, train_X, val_X):
         """``BaseModel.py:192-278``: batch counts, iterators, init, optimizer, sampler."""
@@ -427,10 +435,14 @@ class KGEModel:
 
         def write():
             ev.synchronize()
-            torch.save(snap, path)
+            # a whole file or none: written beside, then renamed onto ckpt.pt
+            # (a reader never sees a half-written checkpoint)
+            torch.save(snap, path + ".tmp")
+            os.replace(path + ".tmp", path)
 
         import threading
-        self._ckpt_thread = threading.Thread(target=write, daemon=True)
+        # not a daemon: an exiting interpreter waits for the file
+        self._ckpt_thread = threading.Thread(target=write)
         self._ckpt_thread.start()
         return path
 

@@ -111,7 +111,10 @@ class ShardedStep:
         (a one-GPU rehearsal of the remote path). Each owner block holds
         ceil(capacity_slack * occurrences / G) + capacity_floor rows; a step
         whose ids overflow a block is skipped on every rank and reported by
-        check_status(). ``batch_hint`` (positives per rank per step) sizes the
+        the next check_status() (a sticky device flag, read and cleared
+        there); a skipped step still advances keras Adam's iteration count
+        (``optimizer.iterations``, hence lr_t), as the host counts steps
+        before the device knows of the overflow. ``batch_hint`` (positives per rank per step) sizes the
         exchange blocks up front, so the owned rows are allocated once, at the
         head of the extended table (no second copy of a shard that fills HBM)."""
         self.model = model
@@ -182,6 +185,9 @@ class ShardedStep:
         self.norm2 = self.red[o:o + 4]
         self.loss = self.red[o + 4:o + 5]
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        # sticky exchange-overflow flag: the max of every step's all-reduced
+        # flag since check_status() last read it (no host sync per step)
+        self.xerr = torch.zeros(1, dtype=torch.float32, device=dev)
         c = getattr(model, "constraint", False)
         self.renorm = self.mid in _RENORM and bool(c)
         self.clip = self.mid in _CLIP and bool(c)
@@ -666,17 +672,27 @@ class ShardedStep:
         small = self.red[-8:]     # [norm^2 x4 | loss | - | - | exchange error flag]
         if split:
             # 3a. score pass, global norms / loss / error, update pass
+            # (prof_events [before K0, before KS, after KS, after KU]: the
+            # score pass records the first three, the update pass the last --
+            # KU's interval then also holds the [norm^2 | loss | flag]
+            # all-reduce between the passes)
+            ev_s = ev_u = None
+            if prof_events is not None:
+                sc = self._scratch_events()
+                ev_s = (ctypes.c_void_p * 4)(prof_events[0], prof_events[1], prof_events[2], sc[0])
+                ev_u = (ctypes.c_void_p * 4)(sc[0], sc[1], sc[2], prof_events[3])
             f = self._split_fused()
             f.tables = lt
             f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_PHASE_SCORE
-            f(lpos, True, optimizer, neg_ids=lneg, prof_events=prof_events)
+            f(lpos, True, optimizer, neg_ids=lneg, prof_events=ev_s)
             small[-1:].copy_(b["err"])
             if G > 1:
                 self.ex.all_reduce(small)
+            torch.maximum(self.xerr, small[-1:], out=self.xerr)
             f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_PHASE_UPDATE
             f.remote_from = self.Es
             f.abort = small[-1:]
-            f(lpos, True, optimizer, neg_ids=lneg)
+            f(lpos, True, optimizer, neg_ids=lneg, prof_events=ev_u)
             if G > 1:
                 self.ex.all_reduce(self.red[:-8])   # relation gradients
             grad_blocks = [blocks]
@@ -692,6 +708,7 @@ class ShardedStep:
             small[-1:].copy_(b["err"])
             if G > 1:
                 self.ex.all_reduce(self.red)
+            torch.maximum(self.xerr, small[-1:], out=self.xerr)
             grad_blocks = gb
         if not is_train:
             return self.loss
@@ -721,6 +738,16 @@ class ShardedStep:
                                     lr=optimizer.learning_rate)
         self._apply_rel(optimizer, abort=small[-1:], extra=dense_items)
         return self.loss
+
+    def _scratch_events(self):
+        """Three recorded HIP events the split step's profiling passes use as
+        placeholders (handles; torch creates an event at its first record)."""
+        if getattr(self, "_sc_ev", None) is None:
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            for e in evs:
+                e.record()
+            self._sc_ev = (evs, [e.cuda_event for e in evs])
+        return self._sc_ev[1]
 
     def _gblocks(self, b):
         """Gradient rows of the fetched blocks [G cap, cols], per entity table."""
@@ -801,7 +828,8 @@ class ShardedStep:
             self.direct.check_status()
         if self.fused is not None:
             _hip.check_device_status(self.status, "kge_step")
-        if self._ext is not None and float(self.red[-1]) != 0.0:
+        if self._ext is not None and float(self.xerr) != 0.0:
+            self.xerr.zero_()
             raise RuntimeError("sparse exchange: the step's ids overflowed an owner block (capacity %d rows); "
                                "the step was skipped on every rank -- raise capacity_slack" % self._ext["cap"])
 

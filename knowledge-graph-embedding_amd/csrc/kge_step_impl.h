@@ -872,8 +872,11 @@ void update_kernel(StepArgs A) {
   // workspace for this plan or refused it (and reported); here a refused
   // workspace just leaves every wave idle -- one scalar compare, no branch
   // of its own (an early return cost the compact instance registers)
-  const bool ws_ok = (!KGE_GUARD_KU || *reinterpret_cast<const uint32_t*>(&A.ctl->plan_sig) == A.sig) &&
-                     !(A.abort_flag && *A.abort_flag != 0.f);   // (split step: a rank's exchange failed)
+  const bool ws_ok = !KGE_GUARD_KU || *reinterpret_cast<const uint32_t*>(&A.ctl->plan_sig) == A.sig;
+  // split step, a rank's exchange failed: no table, gradient or relation
+  // write at all, but every destination's counter / hash slot still goes
+  // back to zero -- the workspace is ready for the next step's score pass
+  const bool abort_ = A.abort_flag && *A.abort_flag != 0.f;
   const uint32_t nneg = A.nkeyneg;
   const uint32_t kmask = (1u << A.kshift) - 1u;
   const uint32_t snap_stride = (uint32_t)(M::NSNAP * A.snap_cols);   // B * stride < 2^32 (plan check)
@@ -1259,6 +1262,10 @@ void update_kernel(StepArgs A) {
       constexpr int r = decltype(rc)::value;
       act[r] = ws_ok && dd * KR + r < (int64_t)A.nkeys && t[r].y != 0xFFFFFFFFu &&
                !(A.rel_only && (int64_t)t[r].x < E_);
+      if (abort_) {   // (the leader's slot: one per destination)
+        if (act[r] && lane == 0 && !A.keep_cnt) A.htab[t[r].z] = 0ull;
+        act[r] = false;
+      }
       one[r] = one_ok && act[r] && (int64_t)t[r].x < E_ && t[r].y < nneg;
       n1[r] = 0u;
       f1[r] = make_float2(0.f, 0.f);
@@ -1313,7 +1320,8 @@ void update_kernel(StepArgs A) {
   } else {
     const bool active = ws_ok && dd < (A.rel_only ? R_ : ndest);
     const int64_t d = dd < R_ ? E_ + dd : dd - R_;
-    run_dest(d, d, 0xFFFFFFFFu, active);
+    if (abort_ && active && lane == 0 && !A.keep_cnt) A.cnt[d] = 0u;
+    run_dest(d, d, 0xFFFFFFFFu, active && !abort_);
   }
   if (A.dense) {
     // ||dense gradient||^2: workgroup partial; partials_norm_kernel (the next

@@ -416,6 +416,88 @@ def train_step(model, weights, pos, neg_ids, score=("lp", 2.0), loss=("hinge", 1
     return out
 
 
+def train_step_chunked(model, weights, pos, neg_ids, score=("lp", 2.0), loss=("hinge", 1.0), lr=0.01,
+                       constraint=True, constraint_weight=1.0, side="h+t", limit=None, clip_norm=5.0, dtype=F64,
+                       chunk=32):
+    """``train_step`` (SGD, training) in chunks of ``chunk`` positives, for
+    full-size cases whose per-triple relation matrices (RESCAL / TransR at C4:
+    [B (1+K), d, d] float64 = 10 GB per lookup) do not fit one autograd graph.
+
+    Same math as ``train_step``: the constraint assigns and term once
+    (``BaseModel.py:319``), then per chunk the scores and its share of the
+    loss (``loss_fn`` with batch_scale = B / chunk: every loss is a sum over
+    positives normalised by the whole batch, SANS' softmax is per positive),
+    and its gradients. Per variable the slices are reduced on the fly: a
+    variable with a dense contribution (the constraint term) accumulates the
+    duplicate-summed tensor and its norm is taken of that; an IndexedSlices
+    variable accumulates both the duplicate-summed rows and the sum of the
+    slice values' squares (TF-2.5 clip_by_norm over the values). The apply is
+    then ``clip_by_norm`` + keras SGD as in ``train_step`` (up to float64
+    summation order)."""
+    W = {k: torch.tensor(np.asarray(v), dtype=dtype) for k, v in weights.items()}
+    names = list(W.keys())
+    pos = np.asarray(pos, dtype=np.int64)
+    B = len(pos)
+    Keff = len(neg_ids) // max(B, 1)
+    neg_ids = np.asarray(neg_ids, dtype=np.int64)
+    cfg = {"constraint": constraint, "constraint_weight": constraint_weight, "limit": limit}
+    acc = {n: torch.zeros_like(W[n]) for n in names}
+    sq = {n: 0.0 for n in names}
+    dense = set()
+    touched = set()
+
+    def collect(lval, L, leaves_only):
+        for w in W.values():
+            w.requires_grad_(True)
+        leaves = [x[2] for x in L.rec]
+        gs = torch.autograd.grad(lval, [W[n] for n in names] + leaves, allow_unused=True)
+        for n, g in zip(names, gs[:len(names)]):
+            if g is not None and not leaves_only:
+                acc[n] += g
+                dense.add(n)
+                touched.add(n)
+        for (n, idx, _), g in zip(L.rec, gs[len(names):]):
+            if g is not None:
+                acc[n].index_add_(0, idx, g)
+                sq[n] += float(torch.sum(g * g))
+                touched.add(n)
+
+    L = _Lookups(W, True)
+    for w in W.values():
+        w.requires_grad_(True)
+    cterm = _constraint(model, W, L, torch.as_tensor(pos), cfg, 1.0)
+    total = 0.0
+    if torch.is_tensor(cterm) and cterm.requires_grad:
+        collect(cterm, L, False)
+        total += float(cterm.detach())
+    ps_all, ns_all = [], []
+    for a in range(0, B, chunk):
+        p = pos[a:a + chunk]
+        c = len(p)
+        negt = corrupt(p, neg_ids[a * Keff:(a + c) * Keff], Keff, side)
+        L = _Lookups(W, True)
+        ps = _score_hrt(model, W, L, p[:, 0], p[:, 1], p[:, 2], score, cfg)
+        ns = _score_hrt(model, W, L, negt[:, 0], negt[:, 1], negt[:, 2], score, cfg)
+        lval = loss_fn(loss, ps, ns, B / c)
+        collect(lval, L, True)
+        total += float(lval.detach())
+        ps_all.append(ps.detach())
+        ns_all.append(ns.detach())
+    out = {"loss": total, "pos_score": torch.cat(ps_all).numpy(), "neg_score": torch.cat(ns_all).numpy(),
+           "norm2": {}}
+    with torch.no_grad():
+        for n in names:
+            w = W[n]
+            w.requires_grad_(False)
+            if n not in touched:
+                continue
+            l2 = float(torch.sum(acc[n] * acc[n])) if n in dense else sq[n]
+            out["norm2"][n] = l2
+            w.add_(acc[n] * (-lr * clip_norm / max(math.sqrt(l2), clip_norm)))
+    out["weights"] = {k: v.detach().numpy() for k, v in W.items()}
+    return out
+
+
 def _adam_step(w, g, lr, b1, b2, eps, slots, name, t, dense):
     """keras Adam on one variable (TF 2.5 OptimizerV2): g is the clipped,
     duplicate-summed gradient (zero on rows no slice touched)."""

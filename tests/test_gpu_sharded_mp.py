@@ -22,8 +22,7 @@ pytestmark = pytest.mark.gpu
 
 def _worker(rank, port, name, loss, opt, steps, mode, loopback, out):
     import torch.distributed as dist
-    import __graft_entry__ as ge
-    ge.build()
+    import __graft_entry__  # noqa: F401  (sys.path; the parent's hiplib fixture built the library)
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=2)
     from KGE import optimizers
     from KGE.sharded import ShardedStep
@@ -80,7 +79,7 @@ _LOSS = {"sans": ("sans", 3.0, 1.0), "hinge": ("hinge", 1.0), "bce": ("bce",), "
     ("TransE", "sans", "sgd", "dense", False),      # replica + one all-reduce
     ("RESCAL", "sqerr", "sgd", "dense", False),     # full-table regulariser, 1/G per rank
 ])
-def test_two_ranks_one_gpu_equal_oracle(name, loss, opt, mode, loopback):
+def test_two_ranks_one_gpu_equal_oracle(hiplib, name, loss, opt, mode, loopback):
     steps = 2
     got, got_loss = _run(name, loss, opt, steps, mode, loopback)
     W, pos, neg = _case(0, name)

@@ -113,7 +113,7 @@ def _init_world1(dist, dev):
 
 def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, idx=torch.int64, train=True,
              seed=11, constraint=True, typed=None, lr=0.05, opt="sgd", flags=0, k=None, pos=None, W=None,
-             oracle_dtype=None, oracle_loss=None):
+             oracle_dtype=None, oracle_loss=None, oracle_chunk=None):
     from KGE import engine, optimizers
     from KGE.ns_strategy import TypedStrategy, UniformStrategy
     dev = _dev()
@@ -145,12 +145,19 @@ def run_case(hiplib, model_name, d, B, K, side, score_fn, loss_fn, E=50, R=7, id
     neg = orc.negatives(pos, K, side, E, seed=seed, plane=plane, i64=i64,
                         sampler="typed" if typed is not None else "uniform", typed=tt)
     lim = getattr(m, "limit", None)
-    ref = orc.train_step(model_name, W, pos, neg, score=_spec_score(getattr(m, "score_fn", None))
-                         if model_name not in ("DistMult", "RESCAL") else ("dot", 0.0),
-                         loss=_spec_loss(loss_fn) if oracle_loss is None else oracle_loss,
-                         lr=lr, constraint=constraint if model_name != "RotatE" else False, side=side, train=train,
-                         limit=lim, optimizer=opt, constraint_weight=getattr(m, "constraint_weight", 1.0),
-                         **({} if oracle_dtype is None else {"dtype": oracle_dtype}))
+    sc = _spec_score(getattr(m, "score_fn", None)) if model_name not in ("DistMult", "RESCAL") else ("dot", 0.0)
+    lo = _spec_loss(loss_fn) if oracle_loss is None else oracle_loss
+    if oracle_chunk:   # full-size cases: the same oracle step, one autograd graph per chunk of positives
+        assert train and opt == "sgd"
+        ref = orc.train_step_chunked(model_name, W, pos, neg, score=sc, loss=lo, lr=lr,
+                                     constraint=constraint if model_name != "RotatE" else False, side=side,
+                                     limit=lim, constraint_weight=getattr(m, "constraint_weight", 1.0),
+                                     chunk=oracle_chunk)
+    else:
+        ref = orc.train_step(model_name, W, pos, neg, score=sc, loss=lo,
+                             lr=lr, constraint=constraint if model_name != "RotatE" else False, side=side, train=train,
+                             limit=lim, optimizer=opt, constraint_weight=getattr(m, "constraint_weight", 1.0),
+                             **({} if oracle_dtype is None else {"dtype": oracle_dtype}))
     got = {k: v.cpu().numpy() for k, v in m.model_weights.items()}
     return ref, got, float(step.loss_out.item()), ps.cpu().numpy(), ns.cpu().numpy(), step, neg
 
@@ -288,6 +295,96 @@ def test_transr_shapes(hiplib, d, k, B, K, side, constraint):
     ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransR", d, B, K, side, score.LpDistancePow(2),
                                           loss.PairwiseHingeLoss(1.0), k=k, constraint=constraint, E=90, R=4)
     check(ref, got, l_, ps, ns)
+
+
+def _fb15k237():
+    z = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data",
+                             "fb15k237_train.npz"))
+    return z["triples"].astype(np.int64), int(z["n_entities"]), int(z["n_relations"])
+
+
+def _c4_batch(B, seed):
+    """B positives drawn from FB15k-237 train_indexed (E = 14,505, R = 237):
+    the relation-grouped passes see ~135 live relations at B = 512 (the C4
+    bench batch's count, profiles/r03e/bench_c4-rescal.json)."""
+    X, E, R = _fb15k237()
+    rng = np.random.default_rng(seed)
+    pos = X[rng.choice(len(X), B, replace=False)]
+    return pos, E, R
+
+
+@pytest.mark.parametrize("B", [512, 128])
+def test_rescal_c4_full_size(hiplib, B):
+    """RESCAL at the C4 shape (RESCAL.py:140-200): d = 200, K = 64 'h+t',
+    SquareError, constraint (dense Lp regulariser over both full tables), SGD,
+    E = 14,505, R = 237, positives real FB15k-237 rows (B = 512: ~135 live
+    relations; the relation rank, per-relation segments, MFMA context / dR
+    strips and the fused dense apply at their bench sizes) vs the float64
+    oracle, chunked by 32 positives (its per-triple R_r lookups would be
+    [B (1+K), d, d] = 10 GB in one graph)."""
+    from KGE import loss
+    pos, E, R = _c4_batch(B, 40 + B)
+    assert len(np.unique(pos[:, 1])) >= (100 if B == 512 else 50)
+    rng = np.random.default_rng(B)
+    W = _weights("RESCAL", E, R, 200, rng)
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "RESCAL", 200, B, 64, "h+t", None, loss.SquareErrorLoss(),
+                                          E=E, R=R, pos=pos, W=W, lr=0.01, oracle_chunk=32)
+    check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("B", [512, 128])
+def test_transr_c4_full_size(hiplib, B):
+    """TransR at the C4 shape (TransR.py:154-211): d = k = 200, K = 64 'h+t',
+    LpDistancePow(2), hinge(1), constraint (table clip + clip of every
+    projected vector), SGD, E = 14,505, R = 237, real FB15k-237 positives
+    (~135 live relations at B = 512: the relation rank, per-positive MFMA
+    products, the dM strips and transr_proj_apply at their bench sizes) vs
+    the float64 oracle, chunked by 32 positives."""
+    from KGE import loss, score
+    pos, E, R = _c4_batch(B, 50 + B)
+    rng = np.random.default_rng(B + 1)
+    W = _weights("TransR", E, R, 200, rng)
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransR", 200, B, 64, "h+t", score.LpDistancePow(2),
+                                          loss.PairwiseHingeLoss(1.0), E=E, R=R, pos=pos, W=W, lr=0.01,
+                                          oracle_chunk=32)
+    check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("model_name", ["RESCAL", "TransR"])
+def test_c4_full_size_properties(hiplib, model_name):
+    """C4 at bench size (B = 512, K = 64, d = 200, FB15k-237 positives):
+    finite loss, the hinge / square-error loss >= 0, and a second identical
+    step from the same state and planes reproduces the first bit for bit
+    (no float atomics in the relation-grouped passes)."""
+    from KGE import engine, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    dev = _dev()
+    pos, E, R = _c4_batch(512, 7)
+    rng = np.random.default_rng(9)
+    W = _weights(model_name, E, R, 200, rng)
+    outs = []
+    for _ in range(2):
+        if model_name == "RESCAL":
+            m = _make("RESCAL", 200, 64, "h+t", None, loss.SquareErrorLoss(), E, R, UniformStrategy(np.arange(E), seed=5))
+        else:
+            m = _make("TransR", 200, 64, "h+t", score.LpDistancePow(2), loss.PairwiseHingeLoss(1.0), E, R,
+                      UniformStrategy(np.arange(E), seed=5))
+        m.model_weights = {k: torch.tensor(v, device=dev) for k, v in W.items()}
+        step = engine.FusedStep(m)
+        ps = torch.zeros(512, device=dev)
+        ns = torch.zeros(512 * 64, device=dev)
+        step(torch.tensor(pos, device=dev), True, optimizers.SGD(0.01), pos_score=ps, neg_score=ns)
+        torch.cuda.synchronize()
+        step.check_status()
+        outs.append((float(step.loss_out.item()), {k: v.clone() for k, v in m.model_weights.items()}, ps, ns))
+    l0 = outs[0][0]
+    assert math.isfinite(l0) and l0 >= 0
+    for k in W:
+        assert bool(torch.isfinite(outs[0][1][k]).all()), k
+        assert torch.equal(outs[0][1][k], outs[1][1][k]), k
+        assert not np.array_equal(outs[0][1][k].cpu().numpy(), W[k]), k
+    assert torch.equal(outs[0][2], outs[1][2]) and torch.equal(outs[0][3], outs[1][3])
+    assert l0 == outs[1][0]
 
 
 def test_transr_validation_and_adam(hiplib):
@@ -907,7 +1004,11 @@ def test_sharded_sparse_adam_world1(hiplib, model_name, loopback):
 def test_sharded_exchange_overflow_voids_step(hiplib, model_name):
     """A step whose ids overflow an owner block (capacity below the step's
     unique ids) is skipped whole -- no table changes -- and check_status()
-    reports it; the next step with room runs normally."""
+    reports it (also when later steps succeed: the flag is sticky until read).
+    The next step with room, same shapes and so the same plan and workspace
+    (no re-zeroing), == the oracle: the voided step left no counters, hash
+    slots or list entries behind. Negatives come from an 8-entity pool, so
+    a batch of positives over those 8 entities fits the 16-row blocks."""
     import torch.distributed as dist
     from KGE import loss, optimizers, score
     from KGE.ns_strategy import UniformStrategy
@@ -916,21 +1017,44 @@ def test_sharded_exchange_overflow_voids_step(hiplib, model_name):
     _init_world1(dist, dev)
     try:
         rng = np.random.default_rng(37)
-        E, R, d, B, K = 300, 4, 24, 32, 8
+        E, R, d, B, K, P = 300, 4, 24, 32, 8, 8
         k = 20 if model_name == "TransR" else None
         W = _weights(model_name, E, R, d, rng, k)
         m = _make(model_name, d, K, "h+t", score.LpDistancePow(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
-                  E, R, UniformStrategy(np.arange(E), seed=6), constraint=False, k=k)
+                  E, R, UniformStrategy(np.arange(P), seed=6), constraint=False, k=k)
         m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
-        st = ShardedStep(m, mode="sparse", local_fast=False, loopback=True, capacity_slack=0.05, capacity_floor=0)
-        pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
-        st(torch.tensor(pos, device=dev), True, optimizers.SGD(0.05))
+        # one rank, every id through the blocks: the split step (TransE: its
+        # update pass aborted) / the grad-mode step (TransR)
+        st = ShardedStep(m, mode="sparse", local_fast=False, loopback=True, capacity_slack=0.05,
+                         capacity_floor=0, batch_hint=B)
+        assert st._ext["cap"] == 16
+        opt = optimizers.SGD(0.05)
+        pos = np.stack([rng.integers(P, E, B), rng.integers(0, R, B), rng.integers(P, E, B)], 1).astype(np.int64)
+        st(torch.tensor(pos, device=dev), True, opt)
         torch.cuda.synchronize()
-        with pytest.raises(RuntimeError, match="overflowed"):
-            st.check_status()
         st.sync()
         for kk, v in W.items():
             np.testing.assert_array_equal(m.model_weights[kk].cpu().numpy(), v, err_msg=kk)
+        # the next steps fit (ids in [0, 8)); the overflow stays reported
+        ref_w = W
+        for it in range(2):
+            pos = np.stack([rng.integers(0, P, B), rng.integers(0, R, B), rng.integers(0, P, B)], 1).astype(np.int64)
+            plane = m.ns_strategy.offset
+            lv = float(st(torch.tensor(pos, device=dev), True, opt))
+            torch.cuda.synchronize()
+            neg = orc.negatives(pos, K, "h+t", P, seed=6, plane=plane)
+            ref = orc.train_step(model_name, ref_w, pos, neg, score=("lppow", 2.0), loss=("sans", 3.0, 1.0), lr=0.05,
+                                 constraint=False)
+            ref_w = ref["weights"]
+            assert abs(lv - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"])), it
+            if it == 0:
+                with pytest.raises(RuntimeError, match="overflowed"):
+                    st.check_status()
+            else:
+                st.check_status()   # read and cleared
+        st.sync()
+        for kk, v in ref_w.items():
+            np.testing.assert_allclose(m.model_weights[kk].cpu().numpy(), v, atol=TOL, err_msg=kk)
     finally:
         dist.destroy_process_group()
 

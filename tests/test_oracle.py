@@ -141,6 +141,34 @@ def test_oracle_gradient_matches_finite_differences(model, score, loss):
             assert abs(fd - g.reshape(-1)[j]) <= 1e-6 * max(1.0, abs(fd)), (name, j, fd, g.reshape(-1)[j])
 
 
+@pytest.mark.parametrize("model,score", FD_MODELS)
+@pytest.mark.parametrize("loss", [("hinge", 1.0), ("logistic",), ("bce",), ("sans", 3.0, 1.0), ("sqerr",)])
+@pytest.mark.parametrize("side", ["h+t", "t"])
+def test_chunked_oracle_equals_one_graph(model, score, loss, side):
+    """train_step_chunked (the full-size C4 checker) == train_step: loss,
+    scores, norms and updated weights, constraints on (TransH / RESCAL dense
+    terms, DistMult's batch term, renormalisation / clip assigns), with a
+    chunk that does not divide B."""
+    from tests.golden.make_golden import case_weights
+    rng = np.random.default_rng(4)
+    E, R, d, B, K = 9, 3, 5, 7, 4
+    W = case_weights(model, E, R, d, rng)
+    pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1)
+    neg = rng.integers(0, E, B * K)
+    kw = dict(score=score, loss=loss, constraint=True, side=side, limit=5.0 / d if model == "RotatE" else None,
+              lr=0.3, constraint_weight=0.4)
+    one = orc.train_step(model, W, pos, neg, **kw)
+    ch = orc.train_step_chunked(model, W, pos, neg, chunk=3, **kw)
+    assert abs(one["loss"] - ch["loss"]) <= 1e-12 * max(1.0, abs(one["loss"]))
+    np.testing.assert_allclose(ch["pos_score"], one["pos_score"], rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(ch["neg_score"], one["neg_score"], rtol=1e-12, atol=1e-14)
+    assert set(ch["norm2"]) == set(one["norm2"])
+    for k in one["norm2"]:
+        assert abs(ch["norm2"][k] - one["norm2"][k]) <= 1e-10 * max(1.0, one["norm2"][k]), k
+    for k, v in one["weights"].items():
+        np.testing.assert_allclose(ch["weights"][k], v, rtol=0, atol=1e-12, err_msg=k)
+
+
 @pytest.mark.parametrize("model", ["TransE", "RESCAL", "TransH"])
 def test_oracle_adam_three_steps_match_eager_plugin_path(model, monkeypatch):
     """keras Adam at t = 1, 2, 3 (BaseModel.py:243-246,328): the oracle's slot
