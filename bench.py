@@ -322,13 +322,21 @@ def cpu_model():
 
 
 def host_cores():
-    """Every core this process may run on (``nproc``: the affinity mask; SURVEY
-    8(d): torch.set_num_threads over all of them). The box's OMP_NUM_THREADS
-    is recorded beside it, not obeyed."""
+    """Every core this process may use (torch.set_num_threads over
+    all of them): the affinity mask, capped by the cgroup's CPU quota (the
+    GPU box: 256 CPUs in the mask, cpu.max "1600000 100000" = 16 CPUs of
+    time -- more threads than that only get throttled). OMP_NUM_THREADS is
+    recorded beside it, not obeyed."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q = cgroup_cpu_max()
+    if q:
+        quota, _, period = q.partition(" ")
+        if quota.isdigit() and period.isdigit() and int(period) > 0:
+            n = min(n, max(1, int(quota) // int(period)))
+    return n
 
 
 def cgroup_cpu_max():
@@ -369,7 +377,8 @@ def cpu_baseline(triples, E, R, B, K, d, budget_s):
     torch.set_num_threads(threads)
     return {"value": n * B / t, "unit": "positive-triples/s", "cores": threads, "kind": "port",
             "single_thread_value": n1 * B / t1, "cpu_model": cpu_model(), "nproc": threads,
-            "cpu_count": os.cpu_count(), "env_omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "env_omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "cgroup_cpu_max": cgroup_cpu_max(),
             "sample": "%d whole C2 steps (B=%d, K=%d, d=%d, FB15k-237) of the fp32 torch-CPU restatement "
                       "(oracle/kge_oracle.py) on %d threads, %.1f s; single thread: %d steps, %.1f s"
@@ -415,7 +424,7 @@ def train_leg(args, dev):
     meta = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
     model = TransE({"embedding_size": d}, K, w["side"], score_fn=w["score"], loss_fn=w["loss"],
                    ns_strategy=UniformStrategy, constraint=w["constraint"])
-    per_epoch = {"histogram": 0.0, "checkpoint": 0.0, "batch_host": 0.0}
+    per_epoch = {"histogram": 0.0, "checkpoint": 0.0, "batch_host": 0.0, "epoch_host": 0.0, "prepare": 0.0}
 
     def timed(name, fn):
         def run(*a, **k):
@@ -424,7 +433,9 @@ def train_leg(args, dev):
             per_epoch[name] += time.perf_counter() - t
             return r
         return run
-    model._log_embeddings_histogram = timed("histogram", model._log_embeddings_histogram)
+    model._histogram_stats = timed("histogram", model._histogram_stats)     # (device statistics, issued)
+    model._finish_epoch = timed("epoch_host", model._finish_epoch)          # (host reads, logs, files)
+    model._prepare_for_train = timed("prepare", model._prepare_for_train)   # (init, iterators, sampler)
     model._save_checkpoint = timed("checkpoint", model._save_checkpoint)
     # host time spent issuing each batch (no sync inside: the GPU runs behind)
     model._run_single_batch = timed("batch_host", model._run_single_batch)
@@ -458,7 +469,8 @@ def train_leg(args, dev):
     fused_ms = (time.perf_counter() - t0) * 1e3 / 200
     hist_ms = per_epoch["histogram"] * 1e3 / args.epochs
     ckpt_ms = per_epoch["checkpoint"] * 1e3 / args.epochs
-    loop_ms = (wall * 1e3 - (hist_ms + ckpt_ms) * args.epochs) / steps
+    ephost_ms = per_epoch["epoch_host"] * 1e3 / args.epochs
+    loop_ms = (wall * 1e3 - (hist_ms + ckpt_ms + ephost_ms) * args.epochs - per_epoch["prepare"] * 1e3) / steps
     _emit({"metric": "positive-triples/sec through KGEModel.train (wall, whole epochs) at d=%d, FB15k-237" % d,
            "value": round(B / (ms * 1e-3), 1), "unit": "positive-triples/s", "n_gpus": 1, "steps": steps,
            "warmup": nb, "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak",
@@ -470,7 +482,9 @@ def train_leg(args, dev):
                            "host_issue_ms_per_batch": round(per_epoch["batch_host"] * 1e3 / steps, 5),
                            "fused_step_ms": round(fused_ms, 5),
                            "host_overhead_ms_per_batch": round(loop_ms - fused_ms, 5),
-                           "per_epoch_ms": {"histogram": round(hist_ms, 3), "checkpoint": round(ckpt_ms, 3)}},
+                           "per_epoch_ms": {"histogram_issue": round(hist_ms, 3), "checkpoint_issue": round(ckpt_ms, 3),
+                                            "epoch_host": round(ephost_ms, 3)},
+                           "prepare_ms": round(per_epoch["prepare"] * 1e3, 3)},
            "roofline": None, "cpu_baseline": None})
 
 

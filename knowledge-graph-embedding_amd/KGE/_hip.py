@@ -214,6 +214,13 @@ def check_device_status(status_tensor, what="kge"):
     if code == KGE_OK:
         return
     status_tensor.zero_()
+    raise_status_code(code, what)
+
+
+def raise_status_code(code, what="kge"):
+    """The exception of a device status word's value (KGE_OK: none)."""
+    if code == KGE_OK:
+        return
     if code == KGE_ERANGE:
         raise ValueError("%s: entity / relation id out of range (device check)" % what)
     if code == KGE_EINVAL:

@@ -172,6 +172,7 @@ class DeviceBatcher:
         self._out = None
         self._perms = {}   # epoch -> its materialised permutation (device int32 [n])
         self._spare = []
+        self._fast = None  # reused buffer: (e0, e1, entry, perm e0, perm e1, stream) of the last batch
 
     def __iter__(self):
         return self
@@ -183,6 +184,17 @@ class DeviceBatcher:
 
     def __next__(self):
         start, B = self._pos, self.batch_size
+        f = self._fast
+        if f is not None and start // self.n == f[0] and (start + B - 1) // self.n == f[1]:
+            # the common case of a reused buffer: the same epoch pair as the last
+            # batch -- one kge_stream_batch_perm call on the stream that batch used
+            self._pos = start + B
+            self._desc.start = start
+            rc = f[2](self._dref, f[3], f[4], f[0], f[5])
+            if rc:
+                from . import _hip
+                _hip.check(rc, "kge_stream_batch_perm")
+            return self._out
         self._pos += B
         if self.data.is_cuda:
             import ctypes
@@ -225,9 +237,10 @@ class DeviceBatcher:
                         _hip.check(L.kge_stream_permutation(self._dref, e, ctypes.c_void_p(t.data_ptr()), stream),
                                    "kge_stream_permutation")
                         perms[e] = t
-                _hip.check(L.kge_stream_batch_perm(self._dref, ctypes.c_void_p(perms[e0].data_ptr()),
-                                                   ctypes.c_void_p(perms[e1].data_ptr()), e0, stream),
-                           "kge_stream_batch_perm")
+                p0, p1 = ctypes.c_void_p(perms[e0].data_ptr()), ctypes.c_void_p(perms[e1].data_ptr())
+                _hip.check(L.kge_stream_batch_perm(self._dref, p0, p1, e0, stream), "kge_stream_batch_perm")
+                if self.reuse_buffer:   # (the permutation tensors stay in self._perms while e0 / e1 are current)
+                    self._fast = (e0, e1, L.kge_stream_batch_perm, p0, p1, stream)
                 return out
             _hip.check(L.kge_stream_batch(self._dref, stream), "kge_stream_batch")
             return out

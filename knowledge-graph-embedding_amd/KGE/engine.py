@@ -282,6 +282,17 @@ class FusedStep:
             batch = batch.to(torch.int64)
         if not batch.is_contiguous():
             batch = batch.contiguous()
+        d = self._desc_for(batch, is_train, optimizer, neg_ids, pos_score, neg_score)
+        d.prof_events = ctypes.cast(prof_events, ctypes.c_void_p) if prof_events is not None else None
+        d.loss_accum = (accum if accum is not None else self.loss_accum).data_ptr()
+        _hip.check(self.lib.kge_step(d, _hip.stream_handle(self.device)), "kge_step")
+        if is_train and isinstance(optimizer, _opt.Adam) and not self.grad_mode:
+            self.apply_adam(optimizer)
+        return self.loss_out
+
+    def _desc_for(self, batch, is_train, optimizer, neg_ids=None, pos_score=None, neg_score=None):
+        """The cached descriptor of this call shape, its per-call pointers and
+        sampler planes filled in; the workspace claimed for its plan."""
         m = self.model
         t = self._tables()
         key = (int(batch.shape[0]), batch.dtype, bool(is_train), id(optimizer),
@@ -330,12 +341,43 @@ class FusedStep:
             if len(self._descs) >= 8:
                 self._descs.clear()
             self._descs[key] = (d, sig)   # (the split step alternates two descriptors)
-        d.prof_events = ctypes.cast(prof_events, ctypes.c_void_p) if prof_events is not None else None
+        return d
+
+    def bind(self, batch, is_train, optimizer, accum=None):
+        """A callable running this step again and again on ``batch``'s buffer
+        (the training loop refills it in place; the sampler's planes advance
+        per call), loss added into ``accum``: the descriptor, stream and entry
+        point are resolved once, so a call is one ``kge_step`` (+ keras Adam's
+        apply) with no per-batch key building. Call again after changing the
+        model's tables, plugins or the optimizer's learning rate."""
+        if batch.device != self.device or batch.dtype not in (torch.int32, torch.int64) or \
+                not batch.is_contiguous():
+            raise ValueError("bind: the batch buffer must be a contiguous int32 / int64 tensor on the step's device")
+        ns = self.model.ns_strategy
+        off = ns.offset
+        d = self._desc_for(batch, is_train, optimizer)
+        ns.offset = off   # (the lookup drew planes for a call that is not made)
+        sig = self._ws_sig
+        d.prof_events = None
         d.loss_accum = (accum if accum is not None else self.loss_accum).data_ptr()
-        _hip.check(self.lib.kge_step(d, _hip.stream_handle(self.device)), "kge_step")
-        if is_train and isinstance(optimizer, _opt.Adam) and not self.grad_mode:
-            self.apply_adam(optimizer)
-        return self.loss_out
+        dref = ctypes.byref(d)
+        step = self.lib.kge_step
+        st = _hip.stream_handle(self.device)
+        planes = self._planes
+        adam = is_train and isinstance(optimizer, _opt.Adam) and not self.grad_mode
+
+        def run():
+            if self._ws_sig != sig:   # another plan used the workspace in between
+                self.workspace.zero_()
+                self._ws_sig = sig
+            d.sampler.offset = planes()
+            rc = step(dref, st)
+            if rc:
+                _hip.check(rc, "kge_step")
+            if adam:
+                self.apply_adam(optimizer)
+            return self.loss_out
+        return run
 
     def _apply_desc(self, var, grad, norm2_ptr, optimizer, name, abort):
         a = _hip.kge_apply_desc()

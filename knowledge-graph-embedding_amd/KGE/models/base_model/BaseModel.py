@@ -111,7 +111,18 @@ class KGEModel:
 
     def _train_epochs(self, epochs, train_iter, val_iter, early_stopping_rounds, restore_best_weight,
                       train_loss_history, val_loss_history, patience_count):
-        """The epoch loop of ``BaseModel.py:100-184``."""
+        """The epoch loop of ``BaseModel.py:100-184``.
+
+        Single-GPU fused training without early stopping never lets the GPU
+        run dry at an epoch boundary: the epoch's loss sums, status word and
+        weight histograms are computed on the stream and copied into pinned
+        host buffers behind its last batch, and the host reads them (logs,
+        loss history, status check) only after it has queued the next epoch's
+        first batches. The values and the order of everything written are the
+        same as reading them at once; a device error is raised one epoch
+        later. Early stopping reads the validation loss at once (its decision
+        gates the next epoch)."""
+        pending = None
         for i in range(epochs):
             # per-epoch loss sums stay on the device: the fused step adds each
             # batch's loss into them itself (no per-batch host work); the host
@@ -122,19 +133,18 @@ class KGEModel:
                 self._run_single_batch(next(train_iter), is_train=True, accum=train_loss)
                 if val_iter is not None and b < self._batch_count_val:
                     self._run_single_batch(next(val_iter), is_train=False, accum=val_loss)
-            self._check_device_status()
-            train_loss = float(train_loss) / self._batch_count_train
-            train_loss_history.append(train_loss)
-            self._log_scalar("train", train_loss, i)
-            if val_iter is not None:
-                val_loss = float(val_loss) / self._batch_count_val
-                val_loss_history.append(val_loss)
-                self._log_scalar("validation", val_loss, i)
-                logging.info("epoch: %i, train loss: %f, valid loss: %f" % (i, train_loss, val_loss))
-            else:
-                logging.info("epoch: %i, train loss: %f" % (i, train_loss))
-            self._log_embeddings_histogram(i)
-
+                if pending is not None and b >= 15:   # the GPU has this epoch's first batches queued
+                    self._finish_epoch(pending, train_loss_history, val_loss_history)
+                    pending = None
+            if pending is not None:
+                self._finish_epoch(pending, train_loss_history, val_loss_history)
+                pending = None
+            ep = self._end_epoch(i, train_loss, val_loss, val_iter is not None)
+            if early_stopping_rounds is None and ep["deferred"]:
+                self._save_checkpoint()   # (pinned copies on the stream; written by a thread)
+                pending = ep
+                continue
+            self._finish_epoch(ep, train_loss_history, val_loss_history)
             if early_stopping_rounds is not None:
                 assert val_iter is not None, "val_X should be given if want to check early stopping."
                 early_stop, patience_count = self._check_early_stopping(
@@ -145,6 +155,57 @@ class KGEModel:
                     break
             else:
                 self._save_checkpoint()
+        if pending is not None:
+            self._finish_epoch(pending, train_loss_history, val_loss_history)
+
+    def _end_epoch(self, i, train_loss, val_loss, has_val):
+        """Queue epoch i's reads behind its last batch: losses, the fused
+        step's status word and the weight histograms' device statistics into
+        pinned host memory, one event after them. Deferred reading only for a
+        single-GPU fused step (multi-GPU keeps its collectives in step)."""
+        fused = self._fused
+        deferred = (self._device.type == "cuda" and isinstance(fused, engine.FusedStep) and _world_size() == 1)
+        ep = {"epoch": i, "has_val": has_val, "deferred": deferred}
+        if not deferred:
+            self._check_device_status()
+            ep["losses"] = (float(train_loss), float(val_loss))
+            ep["hist"] = self._histogram_stats()
+            return ep
+        bufs = self.__dict__.setdefault("_epoch_bufs", {})
+        dev_vals = torch.cat([train_loss, val_loss, fused.status.to(torch.float32)])
+        fused.status.zero_()   # (read from the copy; a later epoch's error is its own)
+        host = bufs.get("vals")
+        if host is None:
+            host = bufs["vals"] = torch.empty(3, dtype=torch.float32, pin_memory=True)
+        host.copy_(dev_vals, non_blocking=True)
+        ep["vals"] = host
+        ep["hist"] = self._histogram_stats(pinned=bufs)
+        ev = torch.cuda.Event()
+        ev.record()
+        ep["event"] = ev
+        return ep
+
+    def _finish_epoch(self, ep, train_loss_history, val_loss_history):
+        """Epoch ep's host side: status check, loss history, logs, histograms."""
+        i = ep["epoch"]
+        if ep["deferred"]:
+            ep["event"].synchronize()
+            tl, vl, code = [float(x) for x in ep["vals"]]
+            from ... import _hip
+            _hip.raise_status_code(int(code), "kge_step")
+        else:
+            tl, vl = ep["losses"]
+        train_loss = tl / self._batch_count_train
+        train_loss_history.append(train_loss)
+        self._log_scalar("train", train_loss, i)
+        if ep["has_val"]:
+            val_loss = vl / self._batch_count_val
+            val_loss_history.append(val_loss)
+            self._log_scalar("validation", val_loss, i)
+            logging.info("epoch: %i, train loss: %f, valid loss: %f" % (i, train_loss, val_loss))
+        else:
+            logging.info("epoch: %i, train loss: %f" % (i, train_loss))
+        self._histogram_write(i, ep["hist"])
 
     def _prepare_for_train(self, train_X, val_X):
         """``BaseModel.py:192-278``: batch counts, iterators, init, optimizer, sampler."""
@@ -179,6 +240,7 @@ class KGEModel:
             self.ns_strategy = TypedStrategy(pool=None, metadata={
                 "type2inds": self.metadata["type2inds"], "ind2type": self.metadata["ind2type"]}, seed=self.seed)
         self._fused = None
+        self.__dict__.pop("_bound", None)
         return train_iter, val_iter
 
     def _to_device(self):
@@ -203,8 +265,21 @@ class KGEModel:
     def _run_single_batch(self, batch_data, is_train, accum=None):
         """One batch (``BaseModel.py:293-330``). Returns the loss as a device
         scalar, or, given ``accum`` (device float32 [1]), adds it there and
-        returns None (the fused single-device step adds it in-kernel)."""
+        returns None (the fused single-device step adds it in-kernel).
+
+        The training loop refills one batch buffer in place, so a single-GPU
+        fused step is bound to (buffer, optimizer, accum) once
+        (``FusedStep.bind``) and later batches are one ``kge_step`` call; the
+        binding is dropped when the plugins, the optimizer or the weight
+        tensors change."""
         opt = self._optimizer if is_train else None
+        if accum is not None:
+            b = self.__dict__.get("_bound")
+            if b is not None:
+                run = b.get((id(batch_data), is_train, id(opt), id(accum)))
+                if run is not None and run[0] == self._bind_fingerprint(opt):
+                    run[1]()
+                    return None
         world = _world_size()
         reason = self._plan_for(opt, batch_data.shape[0] // world)
         if reason is None:
@@ -221,7 +296,20 @@ class KGEModel:
                 rank = torch.distributed.get_rank()
                 batch_data = batch_data[rank * (n // world):(rank + 1) * (n // world)]
             if accum is not None and isinstance(self._fused, engine.FusedStep):
-                self._fused(batch_data, is_train, opt, accum=accum)
+                f = self._fused
+                if batch_data.device == f.device and batch_data.dtype in (torch.int32, torch.int64) and \
+                        batch_data.is_contiguous():
+                    run = f.bind(batch_data, is_train, opt, accum=accum)
+                    b = self.__dict__.setdefault("_bound", {})
+                    if len(b) >= 8:
+                        b.clear()
+                    # the entry holds every object whose id it is keyed or checked by
+                    # (batch, optimizer, accum, weights), so no id can be reused while it lives
+                    b[(id(batch_data), is_train, id(opt), id(accum))] = (
+                        self._bind_fingerprint(opt), run, (batch_data, opt, accum, list(self.model_weights.values())))
+                    run()
+                    return None
+                f(batch_data, is_train, opt, accum=accum)
                 return None
             loss = self._fused(batch_data, is_train, opt)
             if accum is not None:
@@ -237,6 +325,13 @@ class KGEModel:
             accum += loss.reshape(1).to(accum.dtype)
             return None
         return loss.to(torch.float64)
+
+    def _bind_fingerprint(self, opt):
+        """What a bound step depends on besides its buffers: the plugins, the
+        weight tensors and the optimizer's learning rate."""
+        return (id(getattr(self, "score_fn", None)), id(self.loss_fn), id(self.ns_strategy), self.negative_ratio,
+                self.corrupt_side, id(self._fused), getattr(opt, "learning_rate", None),
+                tuple(map(id, self.model_weights.values())))
 
     def sync_weights(self):
         """Multi-GPU: gather the entity shards into ``model_weights`` (before evaluation)."""
@@ -319,11 +414,17 @@ class KGEModel:
         raise NotImplementedError("subclass of KGEModel should implement _check_model_weights()")
 
     def _uniform(self, shape, limit, gen):
+        """U(-limit, limit) drawn where the model lives (the generator's device:
+        a 50M-row table is never drawn on the host)."""
         dev = engine.device()
-        return (torch.rand(shape, generator=gen, dtype=torch.float32) * 2 - 1).mul_(limit).to(dev)
+        x = torch.rand(shape, generator=gen, dtype=torch.float32, device=gen.device)
+        return x.mul_(2).sub_(1).mul_(limit).to(dev)
 
     def _generator(self, seed):
-        g = torch.Generator()
+        """The initialisers' seeded generator, on the model's device (identical
+        draws on every rank of a multi-GPU run for the same seed)."""
+        dev = engine.device()
+        g = torch.Generator(device=dev) if dev.type == "cuda" else torch.Generator()
         if seed is not None:
             g.manual_seed(int(seed))
         else:
@@ -353,53 +454,83 @@ class KGEModel:
         written as JSON lines ``log_path/histogram/<name>.jsonl`` (TensorBoard is not installed):
         TensorBoard's bucketing in float64 -- ``bucket_count`` equal-width buckets from min to max
         (a value at max in the last one), or one bucket ``[x - 0.5, x + 0.5]`` when every value is
-        ``x``; ``[left, right, count]`` per bucket. Computed on the weights' device, ``chunk``
-        values at a time (float64 only per chunk: a 50M-row table is never copied whole). With
-        row-sharded entity tables (multi-GPU sparse mode) each rank counts its own shard and the
-        min / max / counts are all-reduced; rank 0 writes the file."""
+        ``x``; ``[left, right, count]`` per bucket. Statistics on the weights' device
+        (``_histogram_stats``), the file on rank 0 (``_histogram_write``)."""
+        self._histogram_write(step, self._histogram_stats(bucket_count, chunk))
+
+    def _histogram_stats(self, bucket_count=30, chunk=1 << 24, pinned=None):
+        """Per weight, float64 [n, min, max, count_0 .. count_{bucket_count-1}] computed on the
+        weights' device with no host synchronisation, ``chunk`` values at a time (float64 only per
+        chunk: a 50M-row table is never copied whole). Counts add 1.0 per value into its bucket
+        (``index_add_``: exact, order-free). With row-sharded entity tables (multi-GPU sparse mode)
+        each rank counts its own shard with the all-reduced min / max and the counts are
+        all-reduced. ``pinned`` (a dict of reusable buffers): the vectors are copied into pinned
+        host memory behind the stream's work (non-blocking) and those are returned."""
         d = torch.distributed
-        dist_on = d.is_available() and d.is_initialized()
-        rank0 = not dist_on or d.get_rank() == 0
         parts = {}
         if self._fused is not None and hasattr(self._fused, "entity_parts"):
             parts = self._fused.entity_parts()     # {name: this rank's rows} (sparse mode only)
-        path = os.path.join(self.log_path, "histogram")
-        if rank0:
-            os.makedirs(path, exist_ok=True)
+        out = {}
         for name, w in self.model_weights.items():
             sharded = name in parts
             x = (parts[name] if sharded else w.detach()).reshape(-1)
-            n = torch.tensor([x.numel()], dtype=torch.float64, device=x.device)
-            lo = torch.tensor([np.inf], dtype=torch.float64, device=x.device)
-            hi = torch.tensor([-np.inf], dtype=torch.float64, device=x.device)
+            dev = x.device
+            n = torch.full((1,), float(x.numel()), dtype=torch.float64, device=dev)
+            lo = torch.full((1,), np.inf, dtype=torch.float64, device=dev)
+            hi = torch.full((1,), -np.inf, dtype=torch.float64, device=dev)
             for c0 in range(0, x.numel(), chunk):
                 a, b = torch.aminmax(x[c0:c0 + chunk])
-                lo = torch.minimum(lo, a.to(torch.float64))
-                hi = torch.maximum(hi, b.to(torch.float64))
+                lo = torch.minimum(lo, a.to(torch.float64).reshape(1))
+                hi = torch.maximum(hi, b.to(torch.float64).reshape(1))
             if sharded:
                 d.all_reduce(n)
                 d.all_reduce(lo, op=d.ReduceOp.MIN)
                 d.all_reduce(hi, op=d.ReduceOp.MAX)
-            total, lo, hi = float(n), float(lo), float(hi)
+            width = (hi - lo) / bucket_count
+            width = torch.where(width > 0, width, torch.ones_like(width))   # (one value: one bucket, below)
+            # bucket k = clamp(floor((x - lo) / width), 0, bc - 1): with y = (x - lo) / width >= 0,
+            # floor(y) >= k <=> y >= k, so ge[k] = #(y >= k) (plain reductions -- no atomics: a
+            # float64 index_add_ of millions of values into 30 bins serialises on 30 addresses)
+            ks = torch.arange(1, bucket_count, dtype=torch.float64, device=dev).unsqueeze(1)
+            ge = torch.zeros(bucket_count - 1, dtype=torch.float64, device=dev)
+            sub = max(1, min(chunk, (1 << 27) // max(bucket_count, 1)))   # bool [bc - 1, sub] <= 128 MB
+            for c0 in range(0, x.numel(), sub):
+                y = (x[c0:c0 + sub].to(torch.float64) - lo) / width
+                ge += (y.unsqueeze(0) >= ks).sum(1, dtype=torch.float64)
+            nl = torch.full((1,), float(x.numel()), dtype=torch.float64, device=dev)   # (this rank's values)
+            counts = torch.cat([nl - ge[:1], ge[:-1] - ge[1:], ge[-1:]]) if bucket_count > 1 else nl
+            if sharded:
+                d.all_reduce(counts)
+            st = torch.cat([n, lo, hi, counts])
+            if pinned is not None and dev.type == "cuda":
+                key = ("hist", name)
+                hb = pinned.get(key)
+                if hb is None or hb.numel() != st.numel():
+                    hb = pinned[key] = torch.empty(st.numel(), dtype=torch.float64, pin_memory=True)
+                hb.copy_(st, non_blocking=True)
+                st = hb
+            out[name] = st
+        return out
+
+    def _histogram_write(self, step, stats):
+        """Rank 0 appends one JSON line per weight from ``_histogram_stats``."""
+        if not _is_rank0():
+            return
+        path = os.path.join(self.log_path, "histogram")
+        os.makedirs(path, exist_ok=True)
+        for name, st in stats.items():
+            v = st.cpu().tolist()
+            total, lo, hi, counts = v[0], v[1], v[2], v[3:]
+            bucket_count = len(counts)
             if total == 0:
                 buckets = []
             elif lo == hi:
                 buckets = [[lo - 0.5, hi + 0.5, total]]
             else:
-                width = (hi - lo) / bucket_count
-                counts = torch.zeros(bucket_count, dtype=torch.float64, device=x.device)
-                for c0 in range(0, x.numel(), chunk):
-                    xc = x[c0:c0 + chunk].to(torch.float64)
-                    idx = torch.clamp(torch.floor((xc - lo) / width).to(torch.int64), max=bucket_count - 1)
-                    counts += torch.bincount(idx, minlength=bucket_count).to(torch.float64)
-                if sharded:
-                    d.all_reduce(counts)
-                counts = counts.cpu().tolist()
                 edges = np.linspace(lo, hi, bucket_count + 1)
                 buckets = [[float(edges[k]), float(edges[k + 1]), counts[k]] for k in range(bucket_count)]
-            if rank0:
-                with open(os.path.join(path, "%s.jsonl" % name), "a") as f:
-                    f.write(json.dumps({"step": step, "buckets": buckets}) + "\n")
+            with open(os.path.join(path, "%s.jsonl" % name), "a") as f:
+                f.write(json.dumps({"step": step, "buckets": buckets}) + "\n")
 
     def _save_checkpoint(self):
         """``CheckpointManager(max_to_keep=1).save()`` (``BaseModel.py:248-253``).

@@ -114,3 +114,65 @@ def test_unsupported_plans_take_plugin_path():
             mm.train(train_X=X, val_X=X, metadata=md, epochs=1, batch_size=4, optimizer="SGD",
                      seed=1, model_weights_initial=None)
         assert np.isfinite(mm.train_loss_history[0])
+
+
+@pytest.mark.parametrize("opt_name", ["SGD", "Adam"])
+def test_train_bound_fast_path_equals_step_sequence(opt_name, tmp_path):
+    """KGEModel.train (BaseModel.py:58-190) on its fast path -- each batch one
+    bound kge_step on the reused batch buffer, epoch reads deferred behind the
+    next epoch's first batches -- equals the plain sequence of FusedStep calls
+    on the same stream of batches: identical weights bit for bit, identical
+    per-epoch losses; every epoch's histogram line equals the host bucketing
+    of that epoch's weights; the checkpoint holds the final weights."""
+    import json as _json
+    from KGE import engine, loss, optimizers, score
+    from KGE.models.translating_based.TransE import TransE
+    from KGE.ns_strategy import UniformStrategy
+    z = np.load(os.path.join(os.path.dirname(GOLD), "..", "data", "fb15k237_train.npz"))
+    X = z["triples"][:700].astype(np.int64)
+    E, R = int(z["n_entities"]), int(z["n_relations"])
+    md = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
+    epochs, B = 3, 64
+
+    def model():
+        return TransE({"embedding_size": 32}, 4, "h+t", score_fn=score.LpDistance(2),
+                      loss_fn=loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), ns_strategy=UniformStrategy,
+                      constraint=True)
+    m = model()
+    m.train(train_X=X, val_X=None, metadata=md, epochs=epochs, batch_size=B, optimizer=opt_name, seed=11,
+            log_path=str(tmp_path))
+    assert m.__dict__.get("_bound"), "the fast path was not taken"
+    # the same run, one FusedStep call per batch
+    m2 = model()
+    m2.metadata, m2.batch_size, m2._model_weights_initial, m2._optimizer = md, B, None, opt_name
+    m2.seed, m2.log_path = 11, str(tmp_path / "ref")
+    it, _ = m2._prepare_for_train(X, None)
+    f = engine.FusedStep(m2)
+    opt = m2._optimizer
+    nb = int(np.ceil(len(X) / B))
+    losses = []
+    hist = []
+    for e in range(epochs):
+        acc = torch.zeros(1, device=f.device)
+        for _ in range(nb):
+            f(next(it), True, opt, accum=acc)
+        losses.append(float(acc) / nb)
+        hist.append({k: v.detach().cpu().numpy().astype(np.float64).reshape(-1) for k, v in m2.model_weights.items()})
+    torch.cuda.synchronize()
+    for k in m.model_weights:
+        assert torch.equal(m.model_weights[k], m2.model_weights[k]), k
+    assert m.train_loss_history == losses
+    for k in m.model_weights:
+        lines = [_json.loads(x) for x in open(tmp_path / "histogram" / ("%s.jsonl" % k))]
+        assert [x["step"] for x in lines] == list(range(epochs))
+        for e, line in enumerate(lines):
+            x = hist[e][k]
+            lo, hi = x.min(), x.max()
+            w = (hi - lo) / 30
+            idx = np.minimum(np.floor((x - lo) / w), 29).astype(np.int64)
+            cnt = np.bincount(idx, minlength=30)
+            edges = np.linspace(lo, hi, 31)
+            assert line["buckets"] == [[float(edges[j]), float(edges[j + 1]), float(cnt[j])] for j in range(30)], (k, e)
+    ck = torch.load(tmp_path / "ckpt.pt", weights_only=True)
+    for k in m.model_weights:
+        assert torch.equal(ck[k], m.model_weights[k].cpu()), k
