@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--force-exchange", action="store_true",
                     help="one GPU: run the multi-GPU step (c5: all-to-all exchange + row cache instead of the "
                          "one-rank shortcut; other workloads: the sharded step with its exchange) as a rehearsal")
+    ap.add_argument("--exchange", default="auto", choices=("auto", "dense", "sparse", "owner"),
+                    help="multi-GPU step (KGE/sharded.py): auto = dense replica up to 1 GiB of entity rows, else "
+                         "owner-side scoring (TransE / DistMult / RotatE) or the sparse row exchange")
     ap.add_argument("--loopback", action="store_true",
                     help="with --force-exchange: every id (own ones too) through the exchange blocks -- the "
                          "remote path's kernels and copies on one GPU")
@@ -596,8 +599,8 @@ def main():
     model, opt = build_model(w, E, R, rank, dev)
     if sharded:
         from KGE.sharded import ShardedStep
-        step = ShardedStep(model, mode="sparse" if w.get("sharded") else "auto",
-                           local_fast=not args.force_exchange, loopback=args.loopback, batch_hint=B)
+        step = ShardedStep(model, mode=args.exchange, local_fast=not args.force_exchange, loopback=args.loopback,
+                           batch_hint=B)
         if E > 10_000_000:
             step.release_entity_tables()   # the shard is the only copy the step needs
     else:

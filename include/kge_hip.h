@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define KGE_ABI_VERSION 5
+#define KGE_ABI_VERSION 6
 
 typedef enum kge_status {
   KGE_OK = 0,
@@ -141,7 +141,35 @@ enum {
    *                 (zero-filled by the call) for the caller to reduce and apply;
    *                 nothing at all when abort_flag is set and *abort_flag != 0. */
   KGE_FLAG_PHASE_SCORE = 32,
-  KGE_FLAG_PHASE_UPDATE = 64
+  KGE_FLAG_PHASE_UPDATE = 64,
+  /* Owner-side scoring (the multi-GPU "owner" step, KGE/sharded.py; TransE /
+   * DistMult / RotatE): entity e lives on rank e mod owner_world, local row
+   * e div owner_world. Each flag is passed with PHASE_SCORE, then (training)
+   * PHASE_UPDATE, same descriptor and workspace:
+   *   OWNER | PHASE_SCORE   batch = owner_world * owner_batch "virtual"
+   *       positives, every rank's (pos = their all-gathered global triples,
+   *       rows of positive v at owner_rows_from + 2v (h) and + 2v + 1 (t) of
+   *       ent). Each draws its slots exactly as its own rank q draws them
+   *       (sampler planes offset + q * (2 for 'h+t', else 1); GIVEN: neg_ids
+   *       [batch * K_eff] all-gathered); the slots whose entity this rank owns
+   *       are scored here and one record per positive is written to
+   *       owner_records (kge_owner_record_floats() floats): partial softmax
+   *       state, loss and slice-norm^2 partials, h / r / t gradient
+   *       accumulators. No update.
+   *   OWNER_MERGE | PHASE_SCORE   batch = owner_batch (this rank's positives,
+   *       pos in ent rows): the owner_world records of each positive
+   *       (owner_records [owner_world, batch, R], source-major) merged into its
+   *       loss, this rank's loss_out / norm2_out shares (the caller all-reduces
+   *       them), its row gradients, and owner_stats_out [batch, 4] (softmax
+   *       max, 1/Z, positive score) that the caller all-gathers.
+   *   OWNER | PHASE_UPDATE   the owned negatives' coefficients from
+   *       owner_stats (all ranks' merge outputs) and their rows' SGD update
+   *       with the clip scales of norm2_out (all-reduced). Run it BEFORE
+   *       OWNER_MERGE | PHASE_UPDATE (whose in-place rows then add to it).
+   *   OWNER_MERGE | PHASE_UPDATE   the positives' rows as the split step's
+   *       update pass (remote_rows_from, relation gradients to grad_out[1]). */
+  KGE_FLAG_OWNER = 128,
+  KGE_FLAG_OWNER_MERGE = 256
 };
 
 typedef struct kge_table {
@@ -258,6 +286,18 @@ typedef struct kge_step_desc {
   /* KGE_FLAG_PHASE_UPDATE (see the flags): */
   int64_t remote_rows_from;   /* entity rows >= this get their raw gradient in place (0: none) */
   const float* abort_flag;    /* device [1]; nonzero: the update pass does nothing (nullable) */
+  /* KGE_FLAG_OWNER / KGE_FLAG_OWNER_MERGE (see the flags): */
+  int32_t owner_world;        /* ranks, >= 1                                    */
+  int32_t owner_rank;         /* this rank                                      */
+  int64_t owner_batch;        /* positives per rank                             */
+  int64_t owner_rows_from;    /* OWNER: rows of virtual positive v: h at owner_rows_from + 2v, t at + 1 */
+  float* owner_records;       /* OWNER: out [batch, R]; OWNER_MERGE: in [owner_world, batch, R] */
+  const float* owner_stats;   /* OWNER | PHASE_UPDATE: [batch, 4] in            */
+  float* owner_stats_out;     /* OWNER_MERGE | PHASE_SCORE: [batch, 4] out      */
+  int64_t owner_key_capacity; /* OWNER: key positions for the owned negatives (0: 5/4 of the
+                                 expected owner_batch * K_eff, + 4096)          */
+  float* owner_err;           /* OWNER: set to 1 when the owned negatives exceed the capacity
+                                 (their keys are dropped: the caller voids the step; nullable) */
 } kge_step_desc;
 
 /*
@@ -493,6 +533,10 @@ uint64_t kge_step_workspace_bytes(const kge_step_desc* d);
  * 0 on error): a workspace stamped with another value must be re-zeroed
  * before this plan uses it (see the ABI rules above). */
 uint32_t kge_step_plan_signature(const kge_step_desc* d);
+
+/* Floats per owner record (KGE_FLAG_OWNER / KGE_FLAG_OWNER_MERGE) of this
+ * descriptor's plan: 16 header floats + 3 gradient-accumulator images (0 on error). */
+int64_t kge_owner_record_floats(const kge_step_desc* d);
 
 /* One training / validation step (see kge_step_desc). */
 kge_status kge_step(const kge_step_desc* d, void* stream);

@@ -11,7 +11,7 @@ import threading
 
 import torch
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 KGE_OK, KGE_EINVAL, KGE_ERANGE, KGE_EHIP, KGE_ENOMEM_WORKSPACE, KGE_EUNSUPPORTED, KGE_EWORKSPACE = range(7)
 
@@ -25,6 +25,8 @@ FLAG_GRAD_ROWS_TOUCHED = 8
 FLAG_GRAD_RENORM = 16
 FLAG_PHASE_SCORE = 32
 FLAG_PHASE_UPDATE = 64
+FLAG_OWNER = 128
+FLAG_OWNER_MERGE = 256
 RANK_TRANS, RANK_ROT, RANK_MUL, RANK_DOT = range(4)
 RANK_FLAG_LANE_PASS = 1
 RPROJ_NONE, RPROJ_HYPER, RPROJ_RANK1 = range(3)
@@ -76,6 +78,10 @@ class kge_step_desc(ctypes.Structure):
         ("shard_rows", ctypes.c_int64), ("global_entities", ctypes.c_int64),
         ("shard_count", ctypes.c_int32), ("_pad3", ctypes.c_int32),
         ("remote_rows_from", ctypes.c_int64), ("abort_flag", ctypes.c_void_p),
+        ("owner_world", ctypes.c_int32), ("owner_rank", ctypes.c_int32),
+        ("owner_batch", ctypes.c_int64), ("owner_rows_from", ctypes.c_int64),
+        ("owner_records", ctypes.c_void_p), ("owner_stats", ctypes.c_void_p), ("owner_stats_out", ctypes.c_void_p),
+        ("owner_key_capacity", ctypes.c_int64), ("owner_err", ctypes.c_void_p),
     ]
 
 
@@ -137,7 +143,7 @@ EXPORTS = ("kge_abi_version", "kge_last_error", "kge_step_workspace_bytes", "kge
            "kge_sample",
            "kge_apply", "kge_apply_many", "kge_constrain_rows", "kge_rank", "kge_apply_rows", "kge_stream_batch",
            "kge_stream_permutation", "kge_stream_batch_perm", "kge_exchange_plan",
-           "kge_exchange_rows")
+           "kge_exchange_rows", "kge_owner_record_floats")
 
 _lock = threading.Lock()
 _lib = None
@@ -160,6 +166,8 @@ def load(path=LIB_PATH):
         L.kge_step_workspace_bytes.argtypes = [ctypes.POINTER(kge_step_desc)]
         L.kge_step_plan_signature.restype = ctypes.c_uint32
         L.kge_step_plan_signature.argtypes = [ctypes.POINTER(kge_step_desc)]
+        L.kge_owner_record_floats.restype = ctypes.c_int64
+        L.kge_owner_record_floats.argtypes = [ctypes.POINTER(kge_step_desc)]
         L.kge_step.restype = ctypes.c_int
         L.kge_step.argtypes = [ctypes.POINTER(kge_step_desc), ctypes.c_void_p]
         L.kge_sample.restype = ctypes.c_int

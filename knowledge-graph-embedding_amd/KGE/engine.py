@@ -169,6 +169,9 @@ class FusedStep:
         self.rel_grad_out = None
         self.abort = None
         self.grad_row_offset = 0      # grad mode: entity gradient buffers start at this table row
+        # owner-side scoring (KGE/sharded.py "owner"): {world, rank, batch, rows_from,
+        # records, stats, stats_out, err, global_entities} of the kge_step_desc owner fields
+        self.owner = None
         self._descs = {}              # call key -> (descriptor, plan signature)
         self._ws_sig = None
 
@@ -261,6 +264,14 @@ class FusedStep:
             d.remote_rows_from = int(self.remote_from)
         if self.abort is not None:
             d.abort_flag = self.abort.data_ptr()
+        if self.owner is not None:
+            o = self.owner
+            d.owner_world, d.owner_rank, d.owner_batch = o["world"], o["rank"], o["batch"]
+            d.owner_rows_from = o.get("rows_from", 0)
+            d.global_entities = o.get("global_entities", 0)
+            for f in ("records", "stats", "stats_out", "err"):
+                if o.get(f) is not None:
+                    setattr(d, "owner_" + f, o[f].data_ptr())
         d.loss_out = self.loss_out.data_ptr()
         d.loss_accum = self.loss_accum.data_ptr()
         d.norm2_out = self.norm2.data_ptr()
@@ -304,7 +315,9 @@ class FusedStep:
                id(m.ns_strategy), m.negative_ratio, m.corrupt_side, self.batch_scale, self.cw_scale, self.flags,
                float(getattr(m, "constraint_weight", 0.0)), self.remote_from, self.grad_row_offset,
                self.rel_grad_out.data_ptr() if self.rel_grad_out is not None else None,
-               self.abort.data_ptr() if self.abort is not None else None)
+               self.abort.data_ptr() if self.abort is not None else None,
+               tuple(sorted((k, v.data_ptr() if torch.is_tensor(v) else v) for k, v in self.owner.items()))
+               if self.owner is not None else None)
         hit = self._descs.get(key)
         if hit is not None:
             d, sig = hit

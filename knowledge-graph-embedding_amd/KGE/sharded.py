@@ -145,23 +145,32 @@ class ShardedStep:
         self.full_reg = self.mid == _hip.MODEL_RESCAL or (self.mid == _hip.MODEL_TRANSH and
                                                            bool(getattr(model, "constraint", False)))
         if mode == "auto":
-            mode = "dense" if E * C * 4 <= DENSE_TABLE_BYTES or self.full_reg else "sparse"
-        if mode not in ("dense", "sparse"):
-            raise ValueError("mode must be 'auto', 'dense' or 'sparse'")
-        if mode == "sparse" and self.full_reg:
+            if E * C * 4 <= DENSE_TABLE_BYTES or self.full_reg:
+                mode = "dense"
+            else:
+                mode = "owner" if self.mid in _SPLIT else "sparse"
+        if mode not in ("dense", "sparse", "owner"):
+            raise ValueError("mode must be 'auto', 'dense', 'sparse' or 'owner'")
+        if mode in ("sparse", "owner") and self.full_reg:
             raise NotImplementedError("sharded step: a full-table regulariser (RESCAL, TransH with constraint) "
                                       "has a dense gradient of every row -- use the dense exchange")
+        if mode == "owner" and self.mid not in _SPLIT:
+            raise NotImplementedError("owner-side scoring covers TransE, DistMult and RotatE")
         self.mode = mode
         self.loopback = bool(loopback)
         self.slack = float(capacity_slack)
         self.cap_floor = int(capacity_floor)
         self._ext = None
         self._needs_loop = False
-        if mode == "sparse":
+        self._own = None
+        if mode in ("sparse", "owner"):
             # owned rows [ent | ent_aux], padded to Es rows (on a GPU: the head of
             # the extended table, the fetched blocks follow -- _ext_for)
             if batch_hint and dev.type == "cuda":
-                self._ext_for(self._occurrences(int(batch_hint)), torch.int64, fill=False)
+                if mode == "owner":   # blocks for the positives' rows + every rank's positive rows
+                    self._ext_for(2 * int(batch_hint), torch.int64, fill=False, pos_rows=2 * G * int(batch_hint))
+                else:
+                    self._ext_for(self._occurrences(int(batch_hint)), torch.int64, fill=False)
             else:
                 self.shard = torch.zeros(self.Es, C, dtype=torch.float32, device=dev)
             self.shard[:self.valid, :self.ce] = ent.reshape(E, -1)[g::G]
@@ -170,7 +179,7 @@ class ShardedStep:
         # the all-reduce buffer: [entity gradients (dense mode) | relation
         # gradients | norm^2 x4 | loss]
         self.rel_roles = [r for r in ("rel", "rel_aux") if t.get(r) is not None]
-        ent_sizes = [E * c for c in self._ecols()] if mode == "dense" else []
+        ent_sizes = [E * c for c in self._ecols()] if mode == "dense" else []   # (sparse / owner: none)
         sizes = [t[r].numel() for r in self.rel_roles]
         self.red = torch.zeros(sum(ent_sizes) + sum(sizes) + 8, dtype=torch.float32, device=dev)
         o = 0
@@ -204,7 +213,7 @@ class ShardedStep:
             if self.full_reg:
                 f.cw_scale = 1.0 / G
             f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT
-            if mode == "sparse":   # every cache row [0, U) is a batch id: no gradient zero-fill
+            if mode != "dense":   # every cache row [0, U) is a batch id: no gradient zero-fill
                 f.flags |= _hip.FLAG_GRAD_ROWS_TOUCHED
             else:   # the replica, global ids, in-register draws from rank-disjoint planes
                 f.plane_fn = lambda ns, n: ns.take_planes(n) * G + g * n
@@ -216,7 +225,7 @@ class ShardedStep:
         # one rank: every row is local, so the fused single-device step runs on
         # the shard itself (in-kernel SGD, compact update launch) -- no cache
         self.direct = None
-        if self.fused is not None and G == 1 and mode == "sparse" and local_fast and not self.loopback:
+        if self.fused is not None and G == 1 and mode != "dense" and local_fast and not self.loopback:
             td = dict(t)
             td["ent"] = self.shard[:, :self.ce].view(self.ent_shape)
             if self.ca:
@@ -235,12 +244,12 @@ class ShardedStep:
         """_constraint_loss assigns (BaseModel.py:319): owned entity rows, and
         the replicated relation tables identically on every rank (dense mode:
         the whole replica)."""
-        rows = self.shard[:self.valid, :self.ce] if self.mode == "sparse" else self._ent_rows(0)
+        rows = self.shard[:self.valid, :self.ce] if self.mode != "dense" else self._ent_rows(0)
         rel = self.tables["rel"]
         if self.fused is not None:
             st = _hip.stream_handle(self.device)
             # (dense mode: kge_step renormalises the replica itself, KGE_FLAG_GRAD_RENORM)
-            if self.renorm and rows.shape[0] and self.mode == "sparse":
+            if self.renorm and rows.shape[0] and self.mode != "dense":
                 _hip.check(self.lib.kge_constrain_rows(_hip.table(rows), 0, 1.0, st), "kge_constrain_rows")
             if self.clip:
                 if rows.shape[0]:
@@ -506,6 +515,8 @@ class ShardedStep:
                         for k, gk in enumerate(self.gent)]
                 self._apply_rel(optimizer, extra=ents)   # every variable in one launch
             return self.loss
+        if self.fused is not None and self.mode == "owner" and (not is_train or isinstance(optimizer, _opt.SGD)):
+            return self._owner_device(batch, is_train, optimizer, neg_ids, prof_events)
         if neg_ids is None:
             neg_ids = self._draw(batch)
         if self.fused is not None:
@@ -533,15 +544,16 @@ class ShardedStep:
         K = int(m.negative_ratio)
         return B * (2 + (2 * (K // 2) if m.corrupt_side == "h+t" else K))
 
-    def _ext_for(self, n_occ, idx_dtype, fill=True):
+    def _ext_for(self, n_occ, idx_dtype, fill=True, pos_rows=0):
         """Fixed-capacity exchange buffers for steps of up to n_occ id
         occurrences (sized once for the largest step seen, so the step's plan
         never changes): the extended table [Es owned rows | G blocks of cap
-        fetched rows] whose head IS the shard, the request / receive id
-        blocks, send rows, the hash table."""
+        fetched rows | pos_rows gathered positive rows (owner mode)] whose
+        head IS the shard, the request / receive id blocks, send rows, the
+        hash table."""
         G = self.G
         old = self._ext
-        if old is not None and old["n_occ"] >= n_occ:
+        if old is not None and old["n_occ"] >= n_occ and old["pos_rows"] >= pos_rows:
             if old["dtype"] != idx_dtype:   # same blocks, id arrays of the other width
                 for k in ("req_ids", "recv_ids"):
                     if k in old:
@@ -551,9 +563,12 @@ class ShardedStep:
                 old["dtype"] = idx_dtype
             return old
         dev, C = self.device, self.C
+        if old is not None:   # (re-planned: keep what the other pass sized for)
+            n_occ = max(n_occ, old["n_occ"])
+            pos_rows = max(pos_rows, old["pos_rows"])
         remote = G > 1 or self.loopback or self._needs_loop
         cap = max(1, int(math.ceil(self.slack * n_occ / G)) + self.cap_floor) if remote else 1
-        rows = self.Es + G * cap
+        rows = self.Es + G * cap + pos_rows
         if dev.type == "cuda" and rows * C * 4 > (1 << 32):
             torch.cuda.empty_cache()   # a shard that fills HBM: hand cached blocks back first
         ext = torch.zeros(rows, C, dtype=torch.float32, device=dev)
@@ -566,7 +581,11 @@ class ShardedStep:
         hs = 1
         while hs < 2 * n_occ:
             hs <<= 1
-        b = {"n_occ": n_occ, "dtype": idx_dtype, "cap": cap, "ext": ext, "hslots": hs,
+        self._own = None   # (its buffers point into the old table)
+        if hasattr(self, "_sf"):
+            self._sf = None
+        b = {"n_occ": n_occ, "dtype": idx_dtype, "cap": cap, "ext": ext, "hslots": hs, "pos_rows": pos_rows,
+             "pos_base": self.Es + G * cap,
              "htab": torch.zeros(hs, dtype=torch.int64, device=dev),
              "req_cnt": torch.zeros(G, dtype=torch.int32, device=dev),
              "req_ids": torch.zeros(G * cap, dtype=idx_dtype, device=dev),
@@ -660,7 +679,7 @@ class ShardedStep:
         x.status = self.status.data_ptr()
         _hip.check(self.lib.kge_exchange_plan(ctypes.byref(x), st), "kge_exchange_plan")
         # 2. requests to the owners, owners gather, rows back
-        blocks = ext[self.Es:]
+        blocks = ext[self.Es:b["pos_base"]]
         if G > 1:
             self.ex.all_to_all(b["recv_cnt"], b["req_cnt"])
             self.ex.all_to_all(b["recv_ids"], b["req_ids"])
@@ -737,6 +756,171 @@ class ShardedStep:
                                     norm2_ptr=self.norm2.data_ptr() + 4 * self._slot(k),
                                     lr=optimizer.learning_rate)
         self._apply_rel(optimizer, abort=small[-1:], extra=dense_items)
+        return self.loss
+
+    # ------------------------------------------------------------ owner-side scoring
+    def _owner_state(self, Bn, idx_dtype, given):
+        """Buffers and the two fused steps of owner mode for Bn positives per
+        rank: extended table [Es | G blocks | 2 G Bn gathered positive rows],
+        records, softmax stats, the all-gathered triples (and negatives)."""
+        G, g = self.G, self.g
+        Keff = self._keff()
+        b = self._ext_for(2 * Bn, idx_dtype, pos_rows=2 * G * Bn)
+        o = self._own
+        if o is not None and o["B"] == Bn and o["dtype"] == idx_dtype and (o["gneg"] is not None) == given:
+            return b, o
+        dev = self.device
+        lt = self._local_tables(b["ext"])
+        fo = engine.FusedStep(self.model, tables=dict(lt))     # the owner pass (virtual batch G Bn)
+        fm = engine.FusedStep(self.model, tables=dict(lt))     # the merge (this rank's Bn)
+        for f in (fo, fm):
+            f.status = self.status
+            f.norm2 = self.norm2                  # merge: this rank's share out; updates: the all-reduced in
+            f.rel_grad_out = self.grel["rel"]     # (the owner pass files no relation keys)
+        fm.loss_out = self.loss
+        fm.batch_scale = float(G)   # (the owner pass's batch is already the global one)
+        fm.remote_from = self.Es
+        fm.plane_fn = lambda ns, n: 0            # (the merge draws nothing)
+        o = {"B": Bn, "dtype": idx_dtype, "fo": fo, "fm": fm, "base_plane": 0,
+             "gtrip": torch.zeros(G * Bn, 3, dtype=idx_dtype, device=dev),
+             "gneg": torch.zeros(G * Bn * Keff, dtype=idx_dtype, device=dev) if given else None,
+             "stats": torch.zeros(G * Bn, 4, dtype=torch.float32, device=dev),
+             "err": torch.zeros(1, dtype=torch.float32, device=dev)}
+        fo.plane_fn = lambda ns, n: o["base_plane"]   # rank 0's planes of this step (set per step)
+        common = {"world": G, "rank": g, "batch": Bn}
+        fo.owner = dict(common, rows_from=b["pos_base"], global_entities=self.E, err=o["err"], stats=o["stats"])
+        fo.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER | _hip.FLAG_PHASE_SCORE
+        # the record width of this plan, then the record buffers
+        probe = fo.describe(o["gtrip"], True, _opt.SGD(0.01), neg_ids=o["gneg"])
+        probe.owner_records = 16   # (non-null placeholder: the query reads no buffer)
+        R = int(self.lib.kge_owner_record_floats(probe))
+        if R <= 0:
+            raise RuntimeError("owner-side scoring: " + self.lib.kge_last_error().decode(errors="replace"))
+        o["R"] = R
+        o["rec"] = torch.zeros(G * Bn, R, dtype=torch.float32, device=dev)
+        o["rec_in"] = torch.zeros(G * Bn, R, dtype=torch.float32, device=dev) if G > 1 else o["rec"]
+        o["stats_mine"] = o["stats"][g * Bn:(g + 1) * Bn]
+        fo.owner["records"] = o["rec"]
+        fm.owner = dict(common, records=o["rec_in"], stats_out=o["stats_mine"])
+        self._own = o
+        return b, o
+
+    def _keff(self):
+        m = self.model
+        K = int(m.negative_ratio)
+        return 2 * (K // 2) if m.corrupt_side == "h+t" else K
+
+    def _owner_device(self, batch, is_train, optimizer, neg_ids, prof_events):
+        """One owner-side-scoring step (KGE_FLAG_OWNER, include/kge_hip.h):
+        the negatives are scored where their rows live, so only positives'
+        rows, per-positive records and small stats cross ranks.
+
+          1. this rank's positives' h / t rows fetched (the exchange plan of
+             2B ids, blocks, all_to_all);
+          2. every rank's positive rows and triples all-gathered;
+          3. owner pass over the G B virtual positives (negatives drawn from
+             each positive's own rank's planes, owned ones scored) -> records;
+          4. all_to_all of the records to the positives' ranks;
+          5. merge -> loss, norm^2 shares, row gradients, softmax stats;
+          6. all-reduce [norm^2 | loss | error flag], all-gather the stats;
+          7. owner update (coefficients, owned rows' SGD) BEFORE
+          8. the positives' rows (own in place, fetched ones' raw gradients);
+          9. relation gradients all-reduced, fetched rows' gradients back to
+             their owners (kge_exchange_rows SGD in rank order); relations
+             applied.
+        Same draws, losses and updates as the single-device step on the
+        concatenated G B batch (up to float summation order)."""
+        G, g = self.G, self.g
+        ex = self.ex
+        Bn = int(batch.shape[0])
+        given = neg_ids is not None
+        b, o = self._owner_state(Bn, batch.dtype, given)
+        cap, ext, C = b["cap"], b["ext"], self.C
+        st = _hip.stream_handle(self.device)
+        loop = self.loopback
+        # 1. the positives' rows: plan (no negatives), requests, owners gather, rows back
+        b["htab"].zero_()
+        b["req_cnt"].zero_()
+        b["err"].zero_()
+        lpos = torch.empty_like(batch)
+        x = _hip.kge_exchange_desc()
+        x.abi_version = _hip.ABI_VERSION
+        x.idx_dtype = _hip.IDX_I64 if batch.dtype == torch.int64 else _hip.IDX_I32
+        x.pos, x.neg = batch.data_ptr(), batch.data_ptr()
+        x.batch, x.n_neg = Bn, 0
+        x.n_entities = self.E
+        x.world, x.rank, x.loopback = G, g, int(loop)
+        x.local_rows = self.Es
+        x.cap = cap
+        x.htab, x.hslots = b["htab"].data_ptr(), b["hslots"]
+        x.pos_out, x.neg_out = lpos.data_ptr(), lpos.data_ptr()
+        x.req_ids, x.req_cnt = b["req_ids"].data_ptr(), b["req_cnt"].data_ptr()
+        x.err_flag = b["err"].data_ptr()
+        x.status = self.status.data_ptr()
+        _hip.check(self.lib.kge_exchange_plan(ctypes.byref(x), st), "kge_exchange_plan")
+        blocks = ext[self.Es:b["pos_base"]]
+        if G > 1:
+            ex.all_to_all(b["recv_cnt"], b["req_cnt"])
+            ex.all_to_all(b["recv_ids"], b["req_ids"])
+            self._xrows(b, _hip.XROWS_GATHER, b["send"], C, self.shard)
+            ex.all_to_all(blocks, b["send"])
+        elif loop:
+            self._xrows(b, _hip.XROWS_GATHER, blocks, C, self.shard)
+        # 2. every rank's positives: rows (h, t of positive v at pos_base + 2v, + 1) and triples
+        P = ext[b["pos_base"]:b["pos_base"] + 2 * G * Bn]
+        mine = P[2 * g * Bn:2 * (g + 1) * Bn]
+        torch.index_select(ext, 0, lpos[:, 0::2].reshape(-1).to(torch.int64), out=mine)
+        ex.all_gather(P, mine)
+        ex.all_gather(o["gtrip"], batch)
+        if given:
+            ex.all_gather(o["gneg"], neg_ids.to(batch.dtype).contiguous())
+        else:
+            m = self.model
+            o["base_plane"] = m.ns_strategy.take_planes(2 if m.corrupt_side == "h+t" else 1) * G
+        # 3. owner pass
+        ev_s = ev_u = None
+        if prof_events is not None:   # [before, owner pass, after it, after the update passes]
+            sc = self._scratch_events()
+            ev_s = (ctypes.c_void_p * 4)(prof_events[0], prof_events[1], prof_events[2], sc[0])
+            ev_u = (ctypes.c_void_p * 4)(sc[0], sc[1], sc[2], prof_events[3])
+        fo, fm = o["fo"], o["fm"]
+        o["err"].zero_()
+        fo.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER | _hip.FLAG_PHASE_SCORE
+        opt = optimizer if is_train else None
+        fo(o["gtrip"], is_train, opt, neg_ids=o["gneg"], prof_events=ev_s)
+        # 4. records to the positives' ranks; 5. merge
+        if G > 1:
+            ex.all_to_all(o["rec_in"], o["rec"])
+        fm.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER_MERGE | _hip.FLAG_PHASE_SCORE
+        fm(lpos, is_train, opt)
+        # 6. [norm^2 x4 | loss | - | - | error flag], the stats
+        small = self.red[-8:]
+        torch.maximum(b["err"], o["err"], out=small[-1:])
+        if G > 1:
+            ex.all_reduce(small)
+            ex.all_gather(o["stats"], o["stats_mine"])
+        torch.maximum(self.xerr, small[-1:], out=self.xerr)
+        if not is_train:
+            return self.loss
+        # 7. the owned negatives' rows, then 8. the positives' rows
+        fo.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER | _hip.FLAG_PHASE_UPDATE
+        fo.abort = small[-1:]
+        fo(o["gtrip"], True, optimizer, neg_ids=o["gneg"], prof_events=ev_u)
+        fm.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER_MERGE | _hip.FLAG_PHASE_UPDATE
+        fm.abort = small[-1:]
+        fm(lpos, True, optimizer)
+        # 9. relation gradients; the fetched rows' gradients back to their owners
+        if G > 1:
+            ex.all_reduce(self.red[:-8])
+        if G > 1 or loop:
+            gk = blocks
+            if G > 1:
+                ex.all_to_all(b["send"], blocks)
+                gk = b["send"]
+            for src in range(G):
+                self._xrows(b, _hip.XROWS_SGD, gk, gk.stride(0), self.shard, source=src,
+                            norm2_ptr=self.norm2.data_ptr(), lr=optimizer.learning_rate)
+        self._apply_rel(optimizer, abort=small[-1:])
         return self.loss
 
     def _scratch_events(self):

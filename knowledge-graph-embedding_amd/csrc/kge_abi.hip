@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <string>
 
+#include "kge_owner.h"
 #include "kge_proj.h"
 
 using namespace kge;
@@ -51,7 +52,8 @@ struct Plan {
   uint64_t o_leaders, o_htab, o_relseg;
   int hbits;
   uint64_t o_gnegp, o_gpos2, o_gdense[3], o_dpart;   // TransH / TransD
-  bool rescal, transr, proj, td, pj_dense;
+  uint64_t o_owncodes;                               // owner-side scoring
+  bool rescal, transr, proj, td, pj_dense, own, omerge;
   uint32_t sig;   // workspace plan signature
 };
 
@@ -162,6 +164,30 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   if (sm.idx_dtype != d->idx_dtype && sm.kind != KGE_SAMPLER_GIVEN)
     return fail(KGE_EINVAL, "sampler idx_dtype must match triples");
 
+  const bool own = d->flags & KGE_FLAG_OWNER, omerge = d->flags & KGE_FLAG_OWNER_MERGE;
+  const bool ph_s = d->flags & KGE_FLAG_PHASE_SCORE, ph_u = d->flags & KGE_FLAG_PHASE_UPDATE;
+  if (own || omerge) {
+    if (own && omerge) return fail(KGE_EINVAL, "KGE_FLAG_OWNER and KGE_FLAG_OWNER_MERGE are exclusive");
+    if (model != KGE_MODEL_TRANSE && model != KGE_MODEL_DISTMULT && model != KGE_MODEL_ROTATE)
+      return fail(KGE_EUNSUPPORTED, "owner-side scoring covers the element-wise family (TransE, DistMult, RotatE)");
+    if (!ph_s && !ph_u) return fail(KGE_EINVAL, "owner-side passes run with KGE_FLAG_PHASE_SCORE or _UPDATE");
+    if (d->owner_world < 1 || d->owner_rank < 0 || d->owner_rank >= d->owner_world || d->owner_batch < 0)
+      return fail(KGE_EINVAL, "owner_world / owner_rank / owner_batch out of range");
+    if (own && d->batch != (int64_t)d->owner_world * d->owner_batch)
+      return fail(KGE_EINVAL, "KGE_FLAG_OWNER: batch must be owner_world * owner_batch");
+    if (omerge && d->batch != d->owner_batch) return fail(KGE_EINVAL, "KGE_FLAG_OWNER_MERGE: batch must be owner_batch");
+    if (d->shard_count > 1) return fail(KGE_EINVAL, "owner-side scoring takes local rows (shard_count <= 1)");
+    if (own && (d->global_entities <= 0 || d->global_entities >= (int64_t)0x7FFFFFFF * d->owner_world))
+      return fail(KGE_EINVAL, "KGE_FLAG_OWNER needs global_entities (the ids' range)");
+    if (own && d->owner_rows_from < 0) return fail(KGE_EINVAL, "owner_rows_from must be >= 0");
+    if (ph_s && d->batch > 0 && !d->owner_records) return fail(KGE_EINVAL, "owner-side passes need owner_records");
+    if (own && ph_u && !d->owner_stats) return fail(KGE_EINVAL, "KGE_FLAG_OWNER | PHASE_UPDATE needs owner_stats");
+    if (omerge && ph_s && !d->owner_stats_out) return fail(KGE_EINVAL, "KGE_FLAG_OWNER_MERGE needs owner_stats_out");
+    if (d->constraint && (model == KGE_MODEL_TRANSE || model == KGE_MODEL_DISTMULT) &&
+        !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT))
+      return fail(KGE_EINVAL, "owner-side scoring needs KGE_FLAG_NO_TABLE_CONSTRAINT (the caller renormalises its shard)");
+  }
+
   Plan& P = *pl;
   P = Plan{};   // every offset defined (the signature hashes them)
   StepArgs& A = P.A;
@@ -209,12 +235,14 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   // workgroup's waves that keeps a wave's share within KGE_SLOTS_PER_WAVE
   // slots, else the whole workgroup -- and kStepWaves / wpp positives per
   // workgroup
+  // (owner pass: a positive streams the ~K_eff / owner_world slots it owns)
+  const int Kw = own ? (int)ceil_div(Keff, d->owner_world) : Keff;
   int wpp = 1;
-  while (wpp < kStepWaves && ((int64_t)wpp * KGE_SLOTS_PER_WAVE < Keff || kStepWaves % wpp != 0)) ++wpp;
+  while (wpp < kStepWaves && ((int64_t)wpp * KGE_SLOTS_PER_WAVE < Kw || kStepWaves % wpp != 0)) ++wpp;
   // small grids (C4: 512 positives x 64 negatives gave 64 workgroups for 256
   // CUs): spread each positive's slots over more waves while the grid has
   // fewer than two workgroups per CU and every wave keeps >= 8 slots
-  while (wpp < kStepWaves && ceil_div(B, kStepWaves / wpp) < 512 && Keff >= 16 * wpp) wpp *= 2;
+  while (wpp < kStepWaves && ceil_div(B, kStepWaves / wpp) < 512 && Kw >= 16 * wpp) wpp *= 2;
   const int nP = kStepWaves / wpp;
   // 'h+t': even slot ranges, so every stream batch starts on an h-corrupt slot
   int SW = std::max<int>(1, (int)ceil_div(Keff, wpp));
@@ -224,7 +252,16 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   // destination keys: codes i*Keff + j (negatives), B*Keff + 3i + c (positive rows)
   const int64_t E = d->ent.rows, R = d->rel.rows;
   const int64_t ndest = rescal ? E : E + R;   // RESCAL's relation gradient comes from the dR pass
-  const int64_t T = B * (Keff + 3);
+  // key positions: the owner pass's owned negatives (a block per workgroup),
+  // the merge pass's positive rows, else every negative + 3 rows per positive
+  int64_t T = B * (Keff + 3);
+  if (own) {
+    T = d->owner_key_capacity > 0 ? d->owner_key_capacity
+                                  : std::min<int64_t>(B * Keff, ceil_div(5 * d->owner_batch * Keff, 4) + 4096);
+    if (T >= (int64_t)0xFFFFFFFF) return fail(KGE_EUNSUPPORTED, "owner key capacity exceeds 32 bits");
+  } else if (omerge) {
+    T = 3 * B;
+  }
   // destination codes: (i << kshift) | j for slot j of positive i, then
   // (B << kshift) + 4 i + c for the positive's own rows (shift-decoded)
   int kshift = 0;
@@ -241,7 +278,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   if (d->flags & KGE_FLAG_DEBUG_LIST_CAP) cap = 4;   // test hook: exercise the overflow path
 
   const int FL = 64 * vec * ncp;
-  const ScoreLds SL = score_lds(FL, nP, Keff);
+  const ScoreLds SL = score_lds(FL, nP, Keff, own);
   P.G.vec = vec;
   P.G.nc = ncp;
   P.G.nWG = (int)nWG;
@@ -348,8 +385,9 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
       if (ps && pu) return fail(KGE_EINVAL, "KGE_FLAG_PHASE_SCORE and KGE_FLAG_PHASE_UPDATE are exclusive");
       if (rescal || transr || proj)
         return fail(KGE_EUNSUPPORTED, "the split step covers the element-wise family (TransE, DistMult, RotatE)");
-      if (d->optimizer != KGE_OPT_SGD) return fail(KGE_EINVAL, "the split step runs KGE_OPT_SGD");
-      if (!d->norm2_out || !d->grad_out[1])
+      const bool own_val = (own || omerge) && ps && d->optimizer == KGE_OPT_NONE;   // owner validation step
+      if (d->optimizer != KGE_OPT_SGD && !own_val) return fail(KGE_EINVAL, "the split step runs KGE_OPT_SGD");
+      if (!own_val && (!d->norm2_out || !d->grad_out[1]))
         return fail(KGE_EINVAL, "the split step needs norm2_out and grad_out[1] (relation gradients)");
       if (fuse_norm_plan) return fail(KGE_EINVAL, "the split step needs KGE_FLAG_NO_TABLE_CONSTRAINT");
     }
@@ -364,6 +402,23 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     }
   }
   A.status = d->status;
+  P.own = own;
+  P.omerge = omerge;
+  if (own || omerge) {
+    A.own_G = d->owner_world;
+    A.own_g = d->owner_rank;
+    A.own_Bq = std::max<int64_t>(d->owner_batch, 1);
+    A.own_planes = d->corrupt_side == KGE_SIDE_HT ? 2 : 1;
+    A.own_rows_from = d->owner_rows_from;
+    A.own_rec = d->owner_records;
+    A.rec_cols = kRecHead + 3 * FL;
+    A.own_stats = d->owner_stats;
+    A.own_stats_out = d->owner_stats_out;
+    A.own_cap = (uint32_t)(own ? T : 0);
+    A.own_err = d->owner_err;
+    A.own_keys = own;
+    A.n_ent = own ? d->global_entities : E;   // (merge: ids are the caller's table rows)
+  }
 
   uint64_t off = 0;
   auto take = [&](uint64_t bytes) { const uint64_t o = off; off += round_up((int64_t)bytes, 256); return o; };
@@ -374,7 +429,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.o_htab = take((uint64_t)(compact ? nlists : 1) * 8);
   P.o_coef = take((uint64_t)(B << kshift) * 8);   // indexed by destination code
   P.o_snap = take((uint64_t)B * nsnap * entc * 4);
-  P.o_gpos = take((uint64_t)B * 3 * rowlen * 4);
+  P.o_gpos = take((uint64_t)(own ? 1 : B * 3 * rowlen) * 4);   // (the owner pass keeps no positive gradients)
   P.o_part = take((uint64_t)((transr || proj) ? std::max<int64_t>(nWG, B) : nWG) * 8 * 4);   // one partial per positive
   P.o_list = take((uint64_t)nlists * cap * 4);
   P.o_ovf = take((uint64_t)T * 8);
@@ -413,6 +468,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
       P.o_dpart = take((uint64_t)kPjDenseWGs * 4 * 4);
     }
   }
+  if (own) P.o_owncodes = take((uint64_t)T * 4);
   P.ws_bytes = std::max<uint64_t>(off, 256);
   // the plan's workspace signature (kge_hip.h): FNV-1a over everything that
   // decides where a counter, list or ticket lives and what it means
@@ -424,7 +480,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
                          (int64_t)P.o_cnt, (int64_t)P.o_htab, (int64_t)P.o_coef, (int64_t)P.o_snap,
                          (int64_t)P.o_gpos, (int64_t)P.o_part, (int64_t)P.o_list, (int64_t)P.o_ovf,
                          (int64_t)P.o_upart, (int64_t)P.o_leaders, (int64_t)P.o_sorted, (int64_t)P.o_relseg,
-                         (int64_t)P.o_gneg, (int64_t)P.o_dpart};
+                         (int64_t)P.o_gneg, (int64_t)P.o_dpart, (int64_t)P.o_owncodes, T,
+                         (int64_t)d->owner_world, (int64_t)d->owner_batch};
     uint32_t h = 2166136261u;
     for (const int64_t v : f)
       for (int b = 0; b < 8; ++b) h = (h ^ (uint32_t)((uint64_t)v >> (8 * b) & 0xFF)) * 16777619u;
@@ -609,6 +666,12 @@ uint32_t kge_step_plan_signature(const kge_step_desc* d) {
   return P.sig;
 }
 
+int64_t kge_owner_record_floats(const kge_step_desc* d) {
+  Plan P;
+  if (make_plan(d, &P) != KGE_OK) return 0;
+  return P.A.rec_cols > 0 ? P.A.rec_cols : kRecHead + 3 * 64 * P.G.vec * P.G.nc;
+}
+
 kge_status kge_step(const kge_step_desc* d, void* stream) {
   Plan P;
   kge_status s = make_plan(d, &P);
@@ -635,6 +698,35 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   A.gpe = A.gpos;
   A.gpe_stride = 3 * A.gcols;
   A.gpe_toff = 2 * A.gcols;
+  if (P.own) A.own_codes = (uint32_t*)(ws + P.o_owncodes);
+  if (P.own || P.omerge) {
+    // owner-side scoring: OWNER | SCORE (owner pass), OWNER | UPDATE
+    // (coefficients + the owned rows' update), OWNER_MERGE | SCORE (merge),
+    // OWNER_MERGE | UPDATE (the positives' rows: the split step's update pass)
+    hipEvent_t const* ev = (hipEvent_t const*)d->prof_events;
+    if (ev) { (void)hipEventRecord(ev[0], st); (void)hipEventRecord(ev[1], st); }
+    const bool upd = d->flags & KGE_FLAG_PHASE_UPDATE;
+    if (d->batch > 0) {
+      if (P.omerge && upd)   // its relation gradients start from zero
+        (void)hipMemsetAsync(d->grad_out[1], 0, (size_t)A.rel.rows * A.rel_gcols * sizeof(float), st);
+      const int phase = upd ? 1 : P.own ? 0 : 2;
+      if (!upd || P.own) {
+        s = d->model == KGE_MODEL_TRANSE ? launch_owner_transe(A, P.G, P.sk, phase, st)
+                                         : launch_owner_other(A, P.G, d->model, P.sk, phase, st);
+        if (s != KGE_OK) return fail(s, "no owner-pass instance for model %d / score %d", d->model, P.sk);
+      }
+      if (ev && !upd) (void)hipEventRecord(ev[2], st);
+      if (upd) {
+        A.run_score = false;
+        s = launch_step_elementwise(A, P.G, d->model, P.sk, st, ev);
+        if (s != KGE_OK) return fail(s, "no kernel instance for model %d / score %d", d->model, P.sk);
+      }
+    } else if (!upd) {
+      (void)hipMemsetAsync(d->loss_out, 0, sizeof(float), st);
+    }
+    if (ev) (void)hipEventRecord(ev[3], st);
+    return hip_check(P.own ? "kge_step(owner pass)" : "kge_step(owner merge)");
+  }
   RelArgs RA{};
   TrArgs TA{};
   if (P.transr) {

@@ -45,6 +45,9 @@ struct StepCtl {
   float reg_r2;            // RESCAL train step: sum_r ||R_r||_F^2 (rel_dr partials)
   uint32_t plan_sig;       // signature of the plan that last used the workspace (0: fresh)
   uint32_t pad1;
+  uint32_t own_count;      // owner score pass: key positions taken (per-workgroup blocks)
+  uint32_t own_len;        // ... handed to the coefficient / update passes by the last workgroup
+  uint32_t pad2[2];
 };
 
 // Workspace plan guard (include/kge_hip.h, "workspace"). Every kernel of a
@@ -203,7 +206,27 @@ struct StepArgs {
   bool rel_grad = false;           // update pass: relation rows' raw gradients -> grel (no update)
   int64_t remote_from = INT64_MAX; // entity rows >= this: raw gradient written in place of the row
   const float* abort_flag = nullptr;   // update pass does nothing when *abort_flag != 0
+  // owner-side scoring (KGE_FLAG_OWNER / KGE_FLAG_OWNER_MERGE; KGE/sharded.py
+  // "owner" mode). The owner pass scores every rank's positives (a virtual
+  // batch of own_G x own_Bq, positive v = q own_Bq + i of rank q) against the
+  // negatives this rank owns (entity e on rank e mod own_G, local row e div
+  // own_G), and leaves per positive one record: its partial softmax state,
+  // loss / norm partials and the h / r / t gradient accumulators. The merge
+  // pass (the positive's rank) combines the records of every owner.
+  int32_t own_G = 1, own_g = 0;
+  int64_t own_Bq = 0;
+  int32_t own_planes = 1;           // sampler planes a rank's step draws from
+  int64_t own_rows_from = 0;        // owner: virtual positive v's h / t rows at own_rows_from + 2 v (+ 1)
+  float* own_rec = nullptr;         // owner: [B, rec_cols] out; merge: [own_G, B, rec_cols] in (source-major)
+  int32_t rec_cols = 0;             // 16 header floats + 3 accumulator images of FL floats
+  const float* own_stats = nullptr; // owner update: [B, 4] (Ms, 1/Z, positive score, -) per virtual positive
+  float* own_stats_out = nullptr;   // merge: [B, 4] out
+  uint32_t* own_codes = nullptr;    // owner: [own_cap] destination code per key position (~0: padding)
+  uint32_t own_cap = 0;             // owner: key positions available (grid of the update launch)
+  float* own_err = nullptr;         // owner: set to 1 when the owned keys exceed own_cap
+  bool own_keys = false;            // update kernel: compact key positions [0, ctl->own_len)
 };
+constexpr int kRecHead = 16;        // owner record: Ms, Z, loss part, hinge / logistic weight, norm^2 x4, -
 
 struct StepGeom {
   int vec, nc;
@@ -361,12 +384,12 @@ __global__ void constrain_rows_kernel(float* t, int64_t rows, int32_t cols, int6
 // Byte offsets of the score kernel's dynamic LDS carve (shared by host and
 // device so the launch size always matches the kernel's view).
 struct ScoreLds {
-  int pos, ids, sR, sT, st, mrg, red, posg, misc, total;
+  int pos, ids, sR, sT, st, mrg, red, posg, misc, jmap, total;
 };
 
 __host__ __device__ inline int lds_align16(int x) { return (x + 15) & ~15; }
 
-__host__ __device__ inline ScoreLds score_lds(int FL, int nP, int Keff) {
+__host__ __device__ inline ScoreLds score_lds(int FL, int nP, int Keff, bool own = false) {
   ScoreLds L;
   int o = 0;
   L.pos = o;  o += lds_align16(nP * 3 * 8);
@@ -378,6 +401,7 @@ __host__ __device__ inline ScoreLds score_lds(int FL, int nP, int Keff) {
   L.red = o;  o += lds_align16(kStepWaves * 3 * FL * 4);
   L.posg = o; o += lds_align16(nP * 3 * FL * 4);
   L.misc = o; o += lds_align16(kStepWaves * 8 * 4);
+  L.jmap = o; o += lds_align16(own ? 2 * nP * Keff * 4 : 0);   // owner pass: compacted slot -> slot | -> row
   L.total = o;
   return L;
 }

@@ -138,7 +138,7 @@ __device__ __forceinline__ float neg_coef(const StepArgs& A, float s, float sp, 
 // positives' keys first (they hold the longest lists -- relation rows,
 // skewed entities -- which then start early instead of forming the update
 // launch's tail), then the negatives'
-__device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_t code) {
+__device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_t code, uint32_t kpos_own = ~0u) {
   uint32_t r;
   int64_t li = dest;   // list index
   if (A.compact) {
@@ -151,7 +151,9 @@ __device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_
       h = (h + 1u) & A.hmask;
     }
     li = h;
-    const uint32_t kpos = code < A.nkeyneg
+    // (the owner pass hands each key its position in the workgroup's block)
+    const uint32_t kpos = kpos_own != ~0u ? kpos_own
+        : code < A.nkeyneg
         ? A.npos3 + (code >> A.kshift) * (uint32_t)A.Keff + (code & ((1u << A.kshift) - 1u))
         : 3u * ((code - A.nkeyneg) >> 2) + ((code - A.nkeyneg) & 3u);
     A.leaders[kpos] = make_uint4((uint32_t)dest, r == 0u ? code : 0xFFFFFFFFu, h, 0u);
@@ -195,6 +197,28 @@ __device__ __forceinline__ int32_t slot_entity(const StepArgs& A, int64_t i, int
     if (A.neg_user) store_idx(A.neg_user, i * A.Keff + j, e, A.i64);
   }
   return (int32_t)ent_row(A, e, err);
+}
+
+// owner pass: slot j of virtual positive v = q * own_Bq + i (rank q's
+// positive i), drawn as rank q's own step draws it -- its planes start at
+// offset + q * own_planes (KGE/sharded.py's rank-disjoint planes) -- or read
+// from the all-gathered given negatives; the local row if this rank owns the
+// entity (e mod own_G == own_g: row e div own_G), else -1
+__device__ __forceinline__ int32_t owner_slot(const StepArgs& A, int64_t v, int j, int* err) {
+  const int64_t q = v / A.own_Bq, i = v - q * A.own_Bq;
+  int kind; uint64_t n, poff;
+  slot_layout(A.side_mode, A.Kside, i, j, &kind, &n, &poff);
+  int64_t e;
+  if (A.given) {
+    e = load_idx(A.neg_user, v * A.Keff + j, A.i64);
+  } else {
+    const int64_t x = load_idx(A.pos, v * 3 + (kind == KIND_HC ? 0 : 2), A.i64);
+    if (A.smp.kind == KGE_SAMPLER_TYPED && (x < 0 || x >= A.n_ent)) { *err = KGE_ERANGE; return -1; }
+    e = sample_entity(A.smp, A.smp.offset + (uint64_t)q * (uint64_t)A.own_planes + poff, n, x, err);
+    if (e < 0) return -1;   // (the sampler reported it)
+  }
+  if (e < 0 || e >= A.n_ent) { *err = KGE_ERANGE; return -1; }
+  return (e % A.own_G) == A.own_g ? (int32_t)(e / A.own_G) : -1;
 }
 
 // compile-time loop over u = 0 .. N-1 (fn gets std::integral_constant<int, u>)
@@ -262,8 +286,10 @@ __device__ void rel_gemv_pair(const float* __restrict__ Rm, int d, int rb, int r
 // per-positive merge slots (LDS)
 enum { MG_F = 0, MG_AP = kMaxWpp, MG_LOSS = kMaxWpp + 1, MG_N = kMaxWpp + 2, MG_UN = kMaxWpp + 8,
        MG_RP = kMaxWpp + 12, MG_TP = kMaxWpp + 13, MG_SP = kMaxWpp + 14, MG_LPP = kMaxWpp + 15,
-       MG_RSQ = kMaxWpp + 16, MG_MS = kMaxWpp + 17, MG_IZ = kMaxWpp + 18, MG_STRIDE = kMergeStride };
-static_assert(MG_IZ < MG_STRIDE, "merge slots exceed the LDS stride");
+       MG_RSQ = kMaxWpp + 16, MG_MS = kMaxWpp + 17, MG_IZ = kMaxWpp + 18,
+       MG_NH = kMaxWpp + 19, MG_KC = kMaxWpp + 20, MG_KB = kMaxWpp + 21,   // owner pass: h slots, slots, key base
+       MG_STRIDE = kMergeStride };
+static_assert(MG_KB < MG_STRIDE, "merge slots exceed the LDS stride");
 
 // ------------------------------------------------------------ KS score
 // One workgroup = kStepWaves waves = nP positives x wpp waves. A wave owns
@@ -277,7 +303,15 @@ static_assert(MG_IZ < MG_STRIDE, "merge slots exceed the LDS stride");
 // positive's waves merge their states through LDS; then every wave
 // finalises its slots' coefficients and files every destination key into
 // that destination's list for the update kernel.
-template <template <int, int, int> class Model, int VEC, int NC, int SK, int SIDE>
+//
+// OWN (KGE_FLAG_OWNER, the multi-GPU owner-side scoring pass): the batch is
+// the virtual batch of every rank's positives; each positive's waves draw its
+// slots from its rank's counter planes, keep the slots whose entity this rank
+// owns, compact them per corruption side (h-corrupt slots, then t-corrupt),
+// stream those, and leave a record (partial softmax state, loss / norm
+// partials, the h / r / t accumulators) instead of finishing the positive;
+// its keys go to per-workgroup blocks of key positions (own_codes).
+template <template <int, int, int> class Model, int VEC, int NC, int SK, int SIDE, bool OWN = false>
 __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((NC >= 2 || Model<VEC, NC, SK>::WIDE) ? KGE_SCORE_WPE_WIDE : KGE_SCORE_WPE))) void score_kernel(StepArgs A) {
   using M = Model<VEC, NC, SK>;
   using F = Frag<VEC, NC>;
@@ -289,7 +323,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
   const int Keff = A.Keff, nP = A.nP, wpp = A.wpp;
-  const ScoreLds L = score_lds(FL, nP, Keff);
+  const ScoreLds L = score_lds(FL, nP, Keff, OWN);
   int64_t* s_pos = reinterpret_cast<int64_t*>(smem + L.pos);
   int32_t* s_ids = reinterpret_cast<int32_t*>(smem + L.ids);
   float* s_R = reinterpret_cast<float*>(smem + L.sR);
@@ -313,8 +347,8 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   const bool active = grp < nValid;
   const int64_t i = i0 + grp;
   const MP mp{A.limit, A.fuse_norm, A.snap + (active ? i : 0) * (M::NSNAP * (int64_t)A.snap_cols)};
-  const int jbeg = min(Keff, gw * A.SW);
-  const int jend = min(Keff, jbeg + A.SW);
+  int jbeg = min(Keff, gw * A.SW);
+  int jend = min(Keff, jbeg + A.SW);
   int32_t* ids = s_ids + grp * Keff;
   float* gR = s_R + grp * Keff;
   float* gT = s_T + grp * Keff;
@@ -323,17 +357,82 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   // workgroup barrier: the slots' ids are read back by this wave only)
   int64_t ph = 0, pr = 0, pt = 0;
   if (active) {
-    ph = load_idx(A.pos, i * 3 + 0, A.i64);
-    pr = load_idx(A.pos, i * 3 + 1, A.i64);
-    pt = load_idx(A.pos, i * 3 + 2, A.i64);
-    ph = ent_row(A, ph, &err);
+    if constexpr (OWN) {
+      // the caller's gathered copies of the positive's rows; its global ids
+      // stay in pos (typed draws, the all-gathered triples)
+      ph = A.own_rows_from + 2 * i;
+      pt = ph + 1;
+      pr = load_idx(A.pos, i * 3 + 1, A.i64);
+    } else {
+      ph = load_idx(A.pos, i * 3 + 0, A.i64);
+      pr = load_idx(A.pos, i * 3 + 1, A.i64);
+      pt = load_idx(A.pos, i * 3 + 2, A.i64);
+      ph = ent_row(A, ph, &err);
+      pt = ent_row(A, pt, &err);
+    }
     if (pr < 0 || pr >= A.rel.rows) { err = KGE_ERANGE; pr = 0; }
-    pt = ent_row(A, pt, &err);
     if (gw == 0 && lane < 3) s_pos[grp * 3 + lane] = lane == 0 ? ph : lane == 1 ? pr : pt;
-    for (int j = jbeg + lane; j < jend; j += KGE_WAVE) ids[j] = slot_entity(A, i, j, &err);
+    if constexpr (OWN) {
+      for (int j = jbeg + lane; j < jend; j += KGE_WAVE) ids[j] = owner_slot(A, i, j, &err);
+    } else {
+      for (int j = jbeg + lane; j < jend; j += KGE_WAVE) ids[j] = slot_entity(A, i, j, &err);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // owner pass: the positive's owned slots compacted by its first wave --
+  // rows into crow, slot numbers into jmap: h-corrupt slots [0, nh), then
+  // t-corrupt [nh, Kc) -- and each wave's ranges of both; the workgroup's
+  // key positions taken in one block (one atomic per workgroup)
+  int hb = 0, he = 0, tb = 0, te = 0;
+  int32_t* jmap = nullptr;
+  if constexpr (OWN) {
+    int32_t* crow = reinterpret_cast<int32_t*>(smem + L.jmap) + nP * Keff + grp * Keff;
+    jmap = reinterpret_cast<int32_t*>(smem + L.jmap) + grp * Keff;
+    float* mgo = s_mrg + grp * MG_STRIDE;
+    __syncthreads();
+    if (active && gw == 0) {
+      int base = 0, nh = 0;
+      for (int pass = 0; pass < (SIDE == KGE_SIDE_HT ? 2 : 1); ++pass) {
+        const int kind = SIDE == KGE_SIDE_HT ? (pass ? KIND_TC : KIND_HC) : kind_at<SIDE>(0);
+        for (int c0 = 0; c0 < Keff; c0 += KGE_WAVE) {
+          const int j = c0 + lane;
+          const int32_t rw = j < Keff ? ids[j] : -1;
+          const bool own = j < Keff && rw >= 0 && slot_kind(A.side_mode, j) == kind;
+          const uint64_t m = __ballot(own);
+          if (own) {
+            const int c = base + __popcll(m & ((1ull << lane) - 1ull));
+            crow[c] = rw;
+            jmap[c] = j;
+          }
+          base += __popcll(m);
+        }
+        if (pass == 0) nh = base;
+      }
+      if (lane == 0) { mgo[MG_NH] = (float)nh; mgo[MG_KC] = (float)base; }
+    }
+    __syncthreads();
+    if (tid == 0) {   // this workgroup's block of key positions
+      int tot = 0;
+      for (int p = 0; p < nValid; ++p) tot += (int)s_mrg[p * MG_STRIDE + MG_KC];
+      const uint32_t b0 = tot ? atomicAdd(&A.ctl->own_count, (uint32_t)tot) : 0u;
+      int o = 0;
+      for (int p = 0; p < nValid; ++p) {
+        s_mrg[p * MG_STRIDE + MG_KB] = __builtin_bit_cast(float, b0 + (uint32_t)o);
+        o += (int)s_mrg[p * MG_STRIDE + MG_KC];
+      }
+    }
+    __syncthreads();
+    ids = crow;
+    if (active) {
+      const int nh = (int)mgo[MG_NH], kc = (int)mgo[MG_KC], nt = kc - nh;
+      const int swh = (nh + wpp - 1) / wpp, swt = (nt + wpp - 1) / wpp;
+      hb = min(nh, gw * swh); he = min(nh, hb + swh);
+      tb = nh + min(nt, gw * swt); te = nh + min(nt, gw * swt + swt);
+    }
+    jbeg = hb;
+    jend = te;
   }
   KGE_PROF(0);
 
@@ -422,6 +521,10 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
     };
     // KGE_SCORE_PREFETCH: the next batch's rows are in flight while this
     // batch is reduced and differentiated (one more batch of registers)
+    // one range [jbeg, jend) of slots whose corruption kinds follow the
+    // pattern S2 (the launch's side; the owner pass: one side per range)
+    auto stream = [&](auto sidec) {
+    constexpr int S2 = decltype(sidec)::value;
     F En[KGE_SCORE_PREFETCH ? ROWS : 1];
     if constexpr (KGE_SCORE_PREFETCH) issue(En, jbeg);
     for (int j0 = jbeg; j0 < jend; j0 += ROWS) {
@@ -448,7 +551,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
       float part[ROWS];
       static_for<ROWS>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
-        M::template fwdk<kind_at<SIDE>(u)>(ctx, E[u], a[u], b[u]);
+        M::template fwdk<kind_at<S2>(u)>(ctx, E[u], a[u], b[u]);
         float pu;
         if constexpr (M::FAST_STREAM) pu = M::template fast_partial<SK>(a[u], b[u]);
         else pu = score_partial<SK, M::CPLX>(a[u], b[u], A.p);
@@ -523,8 +626,19 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
         constexpr int u = decltype(uc)::value;
         const float alu = bcast(al, u << SH);
         const float Mu = SK == SK_PINF ? bcast(Rl, u << SH) : SK == SK_PGEN ? A.p : 0.f;
-        M::template bwdk<kind_at<SIDE>(u)>(ctx, E[u], a[u], b[u], alu, Mu, accH, accR, accT, nrm, mp);
+        M::template bwdk<kind_at<S2>(u)>(ctx, E[u], a[u], b[u], alu, Mu, accH, accR, accT, nrm, mp);
       });
+    }
+    };
+    if constexpr (OWN) {
+      jbeg = hb; jend = he;
+      stream(std::integral_constant<int, SIDE == KGE_SIDE_HT ? KGE_SIDE_H : SIDE>{});
+      if constexpr (SIDE == KGE_SIDE_HT) {
+        jbeg = tb; jend = te;
+        stream(std::integral_constant<int, KGE_SIDE_T>{});
+      }
+    } else {
+      stream(std::integral_constant<int, SIDE>{});
     }
     M::finish(accH, accR, accT);
   }
@@ -554,7 +668,14 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
     }
   }
   // the positive's own gradient at unit alpha (wave 0 of each positive)
-  if (active && gw == 0) {
+  if constexpr (OWN) {
+    // the owner keeps only the context rows its update pass re-derives the
+    // negatives' gradients from, and the positive's score (hinge / logistic)
+    if (active && gw == 0) {
+      if (A.train) M::write_snap(ctx, A.snap + i * (M::NSNAP * (int64_t)A.snap_cols), A.snap_cols);
+      if (lane == 0) s_mrg[grp * MG_STRIDE + MG_SP] = sp;
+    }
+  } else if (active && gw == 0) {
     float* mg = s_mrg + grp * MG_STRIDE;
     float pn[4] = {0.f, 0.f, 0.f, 0.f};
     if (A.train) {
@@ -591,7 +712,35 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   KGE_PROF(2);
 
   // ---- merge the positive's waves (one thread per positive)
-  if (tid < nValid) {
+  if constexpr (OWN) {
+    // the owner's record header: its waves merged at its own reference
+    // maximum (no 1/Z: the positive's rank normalises over every owner)
+    if (tid < nValid) {
+      const int p = tid;
+      float* mg = s_mrg + p * MG_STRIDE;
+      const float* st = s_st + p * wpp * 8;
+      const bool sans = A.loss_kind == KGE_LOSS_SANS;
+      float Ms = -INFINITY;
+      for (int g = 0; g < wpp; ++g) Ms = fmaxf(Ms, st[g * 8]);
+      float Z = 0.f, cw = 0.f, n[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int g = 0; g < wpp; ++g) {
+        const float sc = !sans ? 1.f : (st[g * 8] == -INFINITY ? 0.f : expf(st[g * 8] - Ms));
+        mg[MG_F + g] = sc;
+        Z += st[g * 8 + 1] * sc;
+        cw += st[g * 8 + 3];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) n[v] += sc * sc * st[g * 8 + 4 + v];
+      }
+      mg[MG_MS] = Ms;
+      mg[MG_IZ] = 1.f;
+      float* rec = A.own_rec + (i0 + p) * (int64_t)A.rec_cols;
+      rec[0] = Ms;
+      rec[1] = Z;
+      rec[3] = cw;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) rec[4 + v] = n[v];
+    }
+  } else if (tid < nValid) {
     const int p = tid;
     float* mg = s_mrg + p * MG_STRIDE;
     const float* st = s_st + p * wpp * 8;
@@ -659,7 +808,18 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   KGE_PROF(3);
 
   // ---- the positives' row gradients: sum of the waves' scaled accumulators
-  if (A.train) {
+  if constexpr (OWN) {
+    if (A.train) {   // the record's accumulator images (merged at the owner's maximum)
+      for (int e = tid; e < nValid * 3 * FL; e += blockDim.x) {
+        const int p = e / (3 * FL), rem = e % (3 * FL);
+        const int v = rem / FL, k = rem % FL;
+        const float* mg = s_mrg + p * MG_STRIDE;
+        float sum = 0.f;
+        for (int g = 0; g < wpp; ++g) sum += mg[MG_F + g] * red[((p * wpp + g) * 3 + v) * FL + k];
+        A.own_rec[(i0 + p) * (int64_t)A.rec_cols + kRecHead + v * FL + k] = sum;
+      }
+    }
+  } else if (A.train) {
     for (int e = tid; e < nValid * 3 * FL; e += blockDim.x) {
       const int p = e / (3 * FL), rem = e % (3 * FL);
       const int v = rem / FL, k = rem % FL;
@@ -729,7 +889,43 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   // ---- each wave finalises its slots: loss terms, coefficient, score,
   // destination key (one lane per slot, IEEE transcendentals)
   float lfin = 0.f;
-  if (active) {
+  if constexpr (OWN) {
+    // the owner's loss partial (SANS: at its own maximum, no 1/Z), each owned
+    // slot's (R, ties) for the coefficient pass and its destination key in
+    // the workgroup's block of key positions
+    if (active) {
+      const float* mg = s_mrg + grp * MG_STRIDE;
+      const float Ms = mg[MG_MS], spv = mg[MG_SP];
+      const uint32_t kb = __builtin_bit_cast(uint32_t, mg[MG_KB]);
+      auto fin = [&](int cb, int ce) {
+        for (int c = cb + lane; c < ce; c += KGE_WAVE) {
+          const float R = gR[c];
+          float lp;
+          const float s = score_value<SK>(R, A.pw, &lp, A.p);
+          switch (A.loss_kind) {
+            case KGE_LOSS_HINGE: lfin += fmaxf(A.margin + s - spv, 0.f); break;
+            case KGE_LOSS_LOGISTIC: lfin += logf(1.f + expf(s - spv)); break;
+            case KGE_LOSS_BCE: lfin += log_sigmoid(-s); break;
+            case KGE_LOSS_SANS: lfin += expf(A.temperature * s - Ms) * log_sigmoid(-s - A.margin); break;
+            default: lfin += s * s; break;
+          }
+          if (A.train) {
+            const uint32_t code = ((uint32_t)i << A.kshift) | (uint32_t)jmap[c];
+            A.coef[code] = make_float2(R, gT[c]);
+            const uint32_t kpos = kb + (uint32_t)c;
+            if (kpos < A.own_cap) {
+              A.own_codes[kpos] = code;
+              bin_key(A, ids[c], code, kpos);
+            } else if (A.own_err) {
+              *A.own_err = 1.f;
+            }
+          }
+        }
+      };
+      fin(hb, he);
+      fin(tb, te);
+    }
+  } else if (active) {
     const float* mg = s_mrg + grp * MG_STRIDE;
     const float Ms = mg[MG_MS], invZ = mg[MG_IZ], spv = mg[MG_SP];
     for (int j = jbeg + lane; j < jend; j += KGE_WAVE) {
@@ -757,6 +953,26 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   }
   lfin = wave_sum(lfin);
   if (lane == 0) s_st[wv * 8 + 2] = lfin;   // (merge state already consumed)
+  if constexpr (OWN) {
+    if (err) set_status(A.status, err);
+    __syncthreads();
+    if (tid < nValid) {
+      float l = 0.f;
+      for (int g = 0; g < wpp; ++g) l += s_st[(tid * wpp + g) * 8 + 2];
+      A.own_rec[(i0 + tid) * (int64_t)A.rec_cols + 2] = l;
+    }
+    if (tid == 0) {
+      __builtin_amdgcn_s_waitcnt(0);
+      const uint32_t prev = __hip_atomic_fetch_add(&A.ctl->score_ticket, 1u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == (uint32_t)(gridDim.x - 1)) {   // every workgroup's keys are filed
+        A.ctl->score_ticket = 0u;
+        A.ctl->ovf_len = __hip_atomic_exchange(&A.ctl->ovf_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        A.ctl->own_len = __hip_atomic_exchange(&A.ctl->own_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
+  }
   if (A.train && tid < nValid * 3 && (A.rel_dests || tid % 3 != 2)) {
     const int p = tid / 3, c = tid % 3;
     const int64_t dest = c == 0 ? s_pos[p * 3] : c == 1 ? s_pos[p * 3 + 2] : A.ent.rows + s_pos[p * 3 + 1];
@@ -1248,6 +1464,8 @@ void update_kernel(StepArgs A) {
     // unconditionally: the array is padded to the grid.)
     constexpr int KR = kUpdKeysPerWave;
     const bool one_ok = !A.dense && !A.grad_mode;
+    // (owner pass: the key positions its score pass took)
+    const int64_t nkeys = A.own_keys ? (int64_t)min(A.nkeys, A.ctl->own_len) : (int64_t)A.nkeys;
     uint4 t[KR];
     bool act[KR], one[KR];
     uint32_t n1[KR];
@@ -1260,7 +1478,7 @@ void update_kernel(StepArgs A) {
     });
     static_for<KR>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
-      act[r] = ws_ok && dd * KR + r < (int64_t)A.nkeys && t[r].y != 0xFFFFFFFFu &&
+      act[r] = ws_ok && dd * KR + r < nkeys && t[r].y != 0xFFFFFFFFu &&
                !(A.rel_only && (int64_t)t[r].x < E_);
       if (abort_) {   // (the leader's slot: one per destination)
         if (act[r] && lane == 0 && !A.keep_cnt) A.htab[t[r].z] = 0ull;

@@ -78,6 +78,10 @@ _LOSS = {"sans": ("sans", 3.0, 1.0), "hinge": ("hinge", 1.0), "bce": ("bce",), "
     ("TransE", "sans", "adam", "sparse", False),    # owner ACCUM + dense keras Adam of the shard
     ("TransE", "sans", "sgd", "dense", False),      # replica + one all-reduce
     ("RESCAL", "sqerr", "sgd", "dense", False),     # full-table regulariser, 1/G per rank
+    ("TransE", "sans", "sgd", "owner", False),      # owner-side scoring: records, merge, owner update
+    ("TransE", "hinge", "sgd", "owner", True),
+    ("RotatE", "sans", "sgd", "owner", False),
+    ("DistMult", "bce", "sgd", "owner", False),
 ])
 def test_two_ranks_one_gpu_equal_oracle(hiplib, name, loss, opt, mode, loopback):
     steps = 2

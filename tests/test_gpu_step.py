@@ -905,14 +905,19 @@ def test_fused_adam_three_steps(hiplib, model_name, constraint):
                          [(m, n, s) for m in ("sparse", "loopback", "dense", "local")
                           for n, s in (("TransE", "lp2"), ("TransD", "lppow2"), ("RotatE", "lp1"),
                                        ("TransR", "lppow2"), ("DistMult", None))]
-                         + [("dense", "RESCAL", None), ("dense", "TransH", "lppow2")])
+                         + [("dense", "RESCAL", None), ("dense", "TransH", "lppow2")]
+                         + [(m, n, s) for m in ("owner", "owner-loopback")
+                            for n, s in (("TransE", "lp2"), ("RotatE", "lp1"), ("DistMult", None),
+                                         ("TransE", "lpinf"), ("TransE", "lp3"))])
 def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
     """KGE/sharded.py on the RCCL backend (world size 1): e mod G shard,
     kge_sample draws, the device sparse exchange (kge_exchange_plan ->
     fixed-capacity blocks -> split step or grad-mode step on the extended
     table -> gradient rows back -> kge_exchange_rows; "loopback": every id
     through the blocks, the remote path on one GPU) or the dense replica
-    (grad-mode step, one all-reduce, kge_apply); two steps == two oracle steps
+    (grad-mode step, one all-reduce, kge_apply), or owner-side scoring (the
+    owner pass over the virtual batch with in-kernel draws, records, merge,
+    owner update then the positives' rows); two steps == two oracle steps
     with the same draws."""
     import torch.distributed as dist
     from KGE import loss, optimizers, score
@@ -926,14 +931,14 @@ def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
         k = 20 if model_name in ("TransD", "TransR") else None
         W = _weights(model_name, E, R, d, rng, k)
         sc = {"lp2": score.LpDistance(2), "lppow2": score.LpDistancePow(2), "lp1": score.LpDistance(1),
-              None: None}[score_kind]
+              "lpinf": score.LpDistance(np.inf), "lp3": score.LpDistance(3), None: None}[score_kind]
         m = _make(model_name, d, K, "h+t", sc, loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E, R,
                   UniformStrategy(np.arange(E), seed=9), k=k)
         m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
         # "sparse" forces the exchange + row cache even on one rank; "local" is
         # the one-rank shortcut (the fused step directly on the shard)
-        st = ShardedStep(m, mode="dense" if mode == "dense" else "sparse", local_fast=mode == "local",
-                         loopback=mode == "loopback")
+        st = ShardedStep(m, mode="dense" if mode == "dense" else "owner" if mode.startswith("owner") else "sparse",
+                         local_fast=mode == "local", loopback=mode.endswith("loopback"))
         assert (st.direct is not None) == (mode == "local")
         ref_w = W
         opt = optimizers.SGD(0.05)
