@@ -49,6 +49,7 @@ concatenated G*B batch with the same negatives (up to float summation order).
 import ctypes
 import math
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -515,8 +516,11 @@ class ShardedStep:
                         for k, gk in enumerate(self.gent)]
                 self._apply_rel(optimizer, extra=ents)   # every variable in one launch
             return self.loss
-        if self.fused is not None and self.mode == "owner" and (not is_train or isinstance(optimizer, _opt.SGD)):
-            return self._owner_device(batch, is_train, optimizer, neg_ids, prof_events)
+        if self.mode == "owner" and (not is_train or isinstance(optimizer, _opt.SGD)):
+            if self.fused is not None:
+                return self._owner_device(batch, is_train, optimizer, neg_ids, prof_events)
+            if neg_ids is not None:   # (the host restatement takes the caller's negatives)
+                return self._owner_host(batch, is_train, optimizer, neg_ids)
         if neg_ids is None:
             neg_ids = self._draw(batch)
         if self.fused is not None:
@@ -923,6 +927,190 @@ class ShardedStep:
         self._apply_rel(optimizer, abort=small[-1:])
         return self.loss
 
+    def _score_rows(self, H, Rr, T):
+        """The model's score_hrt on gathered rows (TransE.py:127-155,
+        DistMult.py:118-146, RotatE.py:126-165) -- host restatement."""
+        m = self.model
+        if self.mid == _hip.MODEL_DISTMULT:
+            return torch.sum(H * Rr * T, dim=-1)
+        if self.mid == _hip.MODEL_ROTATE:
+            d = Rr.shape[-1]
+            h2, t2 = H.view(-1, d, 2), T.view(-1, d, 2)
+            th = Rr / m.limit * float(np.float32(np.pi))
+            x = torch.complex(h2[..., 0], h2[..., 1]) * torch.complex(torch.cos(th), torch.sin(th))
+            return m.score_fn(x, torch.complex(t2[..., 0], t2[..., 1]))
+        return m.score_fn(H + Rr, T)
+
+    def _owner_host(self, batch, is_train, optimizer, neg_ids):
+        """Host restatement of ``_owner_device`` (KGE_BACKEND=eager, the gloo
+        CPU tests): the same data flow and the same algebra as the kernels --
+        the owner scores every rank's positives against the negatives it owns
+        and keeps a record per positive (its own softmax maximum Ms_o, Z_o,
+        loss part, hinge / logistic weight sum, slice-norm^2 partials and the
+        h / r / t gradient sums at unit 1/Z); the positive's rank merges the
+        records (Ms = max Ms_o, F_o = exp(Ms_o - Ms), 1/Z); the owners scale
+        their rows' gradients by F_o / Z and apply them. Every per-negative
+        gradient comes from torch autograd on the lookup slices (TF-2.5
+        IndexedSlices), so this checks the merge, not the kernels' calculus."""
+        G, g, ex = self.G, self.g, self.ex
+        m = self.model
+        Bn = int(batch.shape[0])
+        Keff = self._keff()
+        C, ce = self.C, self.ce
+        lk, margin, temp = _loss_kind(m.loss_fn)
+        Bg = float(G * Bn)
+        relt = self.tables["rel"]
+        rel2 = relt.reshape(relt.shape[0], -1)
+        # 1. the positives' rows (the sparse exchange's fetch of 2 Bn ids)
+        ids = torch.cat([batch[:, 0], batch[:, 2]]).to(torch.int64)
+        self._bmax = max(getattr(self, "_bmax", 0), Bn)
+        cache, remap, plan = self._fetch_sparse(ids)
+        hrow, trow = cache[remap[:Bn], :ce], cache[remap[Bn:], :ce]
+        # 2. every rank's positives and negatives
+        gpos = torch.zeros(G * Bn, 2, ce, dtype=torch.float32)
+        ex.all_gather(gpos.view(G * Bn * 2, ce), torch.stack([hrow, trow], 1).reshape(2 * Bn, ce).contiguous())
+        gtri = torch.zeros(G * Bn, 3, dtype=torch.int64)
+        ex.all_gather(gtri, batch.to(torch.int64).contiguous())
+        gneg = torch.zeros(G * Bn * Keff, dtype=torch.int64)
+        ex.all_gather(gneg, neg_ids.to(torch.int64).contiguous())
+        # 3. the owner pass: a record per virtual positive, and its owned rows' gradients
+        R = 8 + 3 * max(ce, rel2.shape[1])
+        rec = torch.zeros(G * Bn, R, dtype=torch.float32)
+        own_rows, own_grad, own_v = [], [], []
+        jk = torch.arange(Keff)
+        hc = (jk % 2 == 0) if m.corrupt_side == "h+t" else torch.full((Keff,), m.corrupt_side == "h")
+        for v in range(G * Bn):
+            e = gneg[v * Keff:(v + 1) * Keff]
+            mine = (e % G) == g
+            sel = torch.nonzero(mine).reshape(-1)
+            h, t, r = gpos[v, 0], gpos[v, 1], rel2[gtri[v, 1]]
+            sp = float(self._score_rows(h[None], r[None], t[None])[0])
+            rec[v, 0] = -math.inf
+            if sel.numel() == 0:
+                continue
+            ish = hc[sel]
+            E = self.shard[torch.div(e[sel], G, rounding_mode="floor"), :ce]
+            Hs = torch.where(ish[:, None], E, h[None].expand_as(E)).clone().requires_grad_(True)
+            Ts = torch.where(ish[:, None], t[None].expand_as(E), E).clone().requires_grad_(True)
+            Rs = r[None].expand(sel.numel(), -1).clone().requires_grad_(True)
+            with torch.enable_grad():
+                sc = self._score_rows(Hs, Rs, Ts)
+                sd = sc.detach()
+                if lk == "sans":
+                    z = temp * sd
+                    Mo = float(z.max())
+                    w = torch.exp(z - Mo)
+                    c = w * torch.sigmoid(sd + margin) / Bg
+                    rec[v, 0], rec[v, 1] = Mo, float(w.sum())
+                    rec[v, 2] = float((w * torch.nn.functional.logsigmoid(-sd - margin)).sum())
+                elif lk == "hinge":
+                    c = (margin + sd - sp >= 0).to(torch.float32) / (Bg * Keff)
+                    rec[v, 2] = float(torch.clamp(margin + sd - sp, min=0).sum())
+                elif lk == "logistic":
+                    c = torch.exp(sd - sp) / (1 + torch.exp(sd - sp))
+                    rec[v, 2] = float(torch.log(1 + torch.exp(sd - sp)).sum())
+                elif lk == "bce":
+                    c = torch.sigmoid(sd) / Bg
+                    rec[v, 2] = float(torch.nn.functional.logsigmoid(-sd).sum())
+                else:
+                    c = sd / Bg
+                    rec[v, 2] = float((sd * sd).sum())
+                rec[v, 3] = float(c.sum())
+                gh, gr, gt = torch.autograd.grad(torch.sum(c * sc), [Hs, Rs, Ts])
+            rec[v, 4] = float((gh * gh).sum() + (gt * gt).sum())
+            rec[v, 5] = float((gr * gr).sum())
+            rec[v, 8:8 + ce] = gh[~ish].sum(0)
+            rec[v, 8 + ce:8 + ce + gr.shape[1]] = gr.sum(0)
+            rec[v, 8 + 2 * ce:8 + 3 * ce] = gt[ish].sum(0)
+            own_rows.append(torch.div(e[sel], G, rounding_mode="floor"))
+            own_grad.append(torch.where(ish[:, None], gh, gt))
+            own_v.append(torch.full((sel.numel(),), v, dtype=torch.int64))
+        # 4. records to the positives' ranks; 5. merge
+        rin = torch.zeros_like(rec)
+        ex.all_to_all(rin, rec)
+        rin = rin.view(G, Bn, R)
+        stats = torch.zeros(G * Bn, 2, dtype=torch.float32)   # (Ms, 1/Z) per virtual positive
+        loss = 0.0
+        n2 = [0.0, 0.0]
+        ggrad = torch.zeros(Bn, 3, C if C >= rel2.shape[1] else rel2.shape[1], dtype=torch.float32)
+        for i in range(Bn):
+            hd = rin[:, i]
+            h = hrow[i].clone().requires_grad_(True)
+            r = rel2[batch[i, 1]].clone().requires_grad_(True)
+            t = trow[i].clone().requires_grad_(True)
+            with torch.enable_grad():
+                spt = self._score_rows(h[None], r[None], t[None])[0]
+                ph, pr, pt = torch.autograd.grad(spt, [h, r, t])
+            sp = float(spt)
+            Ms = float(hd[:, 0].max()) if lk == "sans" else 0.0
+            fo = torch.exp(hd[:, 0] - Ms) if lk == "sans" else torch.ones(G)
+            fo = torch.where(torch.isinf(hd[:, 0]) & (lk == "sans"), torch.zeros_like(fo), fo)
+            Z = float((hd[:, 1] * fo).sum())
+            invZ = (1.0 / Z if Z > 0 else 0.0) if lk == "sans" else 1.0
+            cw = float(hd[:, 3].sum())
+            if lk == "hinge":
+                lossp, cp, wl = 0.0, -cw, 1.0 / (Bg * Keff)
+            elif lk == "logistic":
+                lossp, cp, wl = 0.0, -cw, 1.0
+            elif lk == "bce":
+                lossp = -float(torch.nn.functional.logsigmoid(torch.tensor(sp))) / Bg
+                cp, wl = -float(torch.sigmoid(torch.tensor(-sp))) / Bg, -1.0 / Bg
+            elif lk == "sans":
+                lossp = -float(torch.nn.functional.logsigmoid(torch.tensor(sp + margin))) / Bg
+                cp, wl = -float(torch.sigmoid(torch.tensor(-(sp + margin)))) / Bg, -1.0 / Bg
+            else:
+                lossp, cp, wl = (sp - 1.0) ** 2 * 0.5 / Bg, (sp - 1.0) / Bg, 0.5 / Bg
+            fz = fo * invZ
+            lneg = float(((fz if lk == "sans" else torch.ones(G)) * hd[:, 2]).sum())
+            n2[0] += cp * cp * float((ph * ph).sum() + (pt * pt).sum()) + float((fz * fz * hd[:, 4]).sum())
+            n2[1] += cp * cp * float((pr * pr).sum()) + float((fz * fz * hd[:, 5]).sum())
+            gh = cp * ph + (fz[:, None] * hd[:, 8:8 + ce]).sum(0)
+            grr = cp * pr + (fz[:, None] * hd[:, 8 + ce:8 + ce + pr.shape[0]]).sum(0)
+            gt = cp * pt + (fz[:, None] * hd[:, 8 + 2 * ce:8 + 3 * ce]).sum(0)
+            if self.mid == _hip.MODEL_DISTMULT and getattr(m, "constraint", False):
+                lam = m.constraint_weight
+                rsq = float((r.detach() ** 2).sum())
+                lossp += lam * rsq / Bg
+                grr = grr + (lam / Bg) * 2 * r.detach()
+                n2[1] += float(((lam / Bg) * 2 * r.detach()).pow(2).sum())
+            loss += lossp + wl * lneg
+            ggrad[i, 0, :ce], ggrad[i, 1, :grr.shape[0]], ggrad[i, 2, :ce] = gh, grr, gt
+            stats[g * Bn + i, 0], stats[g * Bn + i, 1] = Ms, invZ
+        # 6. [norm^2 | loss], the stats
+        self.red.zero_()
+        self.norm2[0], self.norm2[1] = n2[0], n2[1]
+        self.loss.fill_(loss)
+        ex.all_reduce(self.red)
+        mine_st = stats[g * Bn:(g + 1) * Bn].clone()
+        ex.all_gather(stats, mine_st)
+        if not is_train:
+            return self.loss
+        lr = optimizer.learning_rate
+        with torch.no_grad():
+            cs0 = 5.0 / max(math.sqrt(float(self.norm2[0])), 5.0)
+            # 7. the owned negatives' rows: gradients at the global softmax state
+            if own_rows:
+                rows = torch.cat(own_rows)
+                vv = torch.cat(own_v)
+                gr_ = torch.cat(own_grad)
+                if lk == "sans":
+                    Mo = rec[vv, 0]
+                    gr_ = gr_ * (torch.exp(Mo - stats[vv, 0]) * stats[vv, 1])[:, None]
+                acc = torch.zeros(self.Es, ce, dtype=torch.float32).index_add_(0, rows, gr_)
+                self.shard[:, :ce] += acc * (cs0 * -lr)
+            # 8. the positives' rows: summed per fetched id, back to their owners
+            gc = torch.zeros(cache.shape[0], ce, dtype=torch.float32)
+            gc.index_add_(0, remap[:Bn], ggrad[:, 0, :ce])
+            gc.index_add_(0, remap[Bn:], ggrad[:, 2, :ce])
+            gbufs = [gc]
+            # relation gradients: this rank's positives, then summed over ranks
+            grel = torch.zeros_like(rel2).index_add_(0, batch[:, 1].to(torch.int64), ggrad[:, 1, :rel2.shape[1]])
+            ex.all_reduce(grel)
+            self.grel["rel"].copy_(grel.view_as(self.grel["rel"]))
+        self._apply_sparse(optimizer, gbufs, *plan)
+        self._apply_rel(optimizer)
+        return self.loss
+
     def _scratch_events(self):
         """Three recorded HIP events the split step's profiling passes use as
         placeholders (handles; torch creates an event at its first record)."""
@@ -1016,6 +1204,21 @@ class ShardedStep:
             self.xerr.zero_()
             raise RuntimeError("sparse exchange: the step's ids overflowed an owner block (capacity %d rows); "
                                "the step was skipped on every rank -- raise capacity_slack" % self._ext["cap"])
+
+
+def _loss_kind(lf):
+    """(kind, margin, temperature) of a built-in loss (loss.py)."""
+    from . import loss as L
+    t = type(lf)
+    if t is L.PairwiseHingeLoss:
+        return "hinge", float(lf.margin), 1.0
+    if t is L.PairwiseLogisticLoss:
+        return "logistic", 0.0, 1.0
+    if t is L.BinaryCrossEntropyLoss:
+        return "bce", 0.0, 1.0
+    if t is L.SelfAdversarialNegativeSamplingLoss:
+        return "sans", float(lf.margin), float(lf.temperature)
+    return "sqerr", 0.0, 1.0
 
 
 def _host_apply(var, grad, norm2, optimizer, name):
