@@ -873,7 +873,7 @@ class ShardedStep:
         # 2. every rank's positives: rows (h, t of positive v at pos_base + 2v, + 1) and triples
         P = ext[b["pos_base"]:b["pos_base"] + 2 * G * Bn]
         mine = P[2 * g * Bn:2 * (g + 1) * Bn]
-        torch.index_select(ext, 0, lpos[:, 0::2].reshape(-1).to(torch.int64), out=mine)
+        mine.copy_(ext.index_select(0, lpos[:, 0::2].reshape(-1).to(torch.int64)))   # (a view of ext: no out=)
         ex.all_gather(P, mine)
         ex.all_gather(o["gtrip"], batch)
         if given:
