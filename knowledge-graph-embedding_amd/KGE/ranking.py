@@ -220,6 +220,23 @@ def filter_index(X, positive_X, side, E):
     entities of the known positives sharing the query's (relation, kept
     entity) -- BaseModel.py:646-650 (mask on r and the kept side), duplicates
     removed (tensor_scatter_nd_update writes -inf once per entity)."""
+    keys, ents = filter_keys(positive_X, side, E)
+    return filter_lookup(X, keys, ents, side, E) + (ents,)
+
+
+def filter_lookup(X, keys, ents, side, E):
+    """[beg, end) of each query's (relation, kept entity) run in ``keys``."""
+    keep = 2 if side == "h" else 0
+    qk = X[:, 1].to(torch.int64) * E + X[:, keep].to(torch.int64)
+    beg = torch.searchsorted(keys, qk, right=False)
+    end = torch.searchsorted(keys, qk, right=True)
+    return beg.contiguous(), end.contiguous()
+
+
+def filter_keys(positive_X, side, E):
+    """The known positives as sorted, unique (relation * E + kept entity,
+    corrupted entity) pairs: ``keys`` ascending, ``ents`` ascending within a
+    key. Independent of the evaluation set, so ``batched_ranks`` caches it."""
     keep, corrupt = (2, 0) if side == "h" else (0, 2)
     P = positive_X.to(torch.int64)
     key = P[:, 1] * E + P[:, keep]            # < R * E: fits int64 for any table
@@ -240,10 +257,40 @@ def filter_index(X, positive_X, side, E):
         if key.numel() > 1:
             first[1:] = (key[1:] != key[:-1]) | (ent[1:] != ent[:-1])
         keys, ents = key[first], ent[first]
-    qk = X[:, 1].to(torch.int64) * E + X[:, keep].to(torch.int64)
-    beg = torch.searchsorted(keys, qk, right=False)
-    end = torch.searchsorted(keys, qk, right=True)
-    return beg.contiguous(), end.contiguous(), ents.contiguous()
+    return keys.contiguous(), ents.contiguous()
+
+
+# evaluate() is called once per epoch (early stopping) and per side with the
+# same positive set: the sorted filter pairs are built once per (content,
+# side, E, device) and kept for the last few sets. The key is the set's bytes
+# hashed on the host (a 272k-triple set: ~1 ms), so an array edited in place
+# is a new set.
+_FILTER_CACHE = {}
+_FILTER_CACHE_MAX = 4
+
+
+def _fingerprint(P):
+    import hashlib
+    a = np.ascontiguousarray(P)
+    try:
+        import xxhash
+        h = xxhash.xxh3_128_hexdigest(a.data)
+    except ImportError:
+        h = hashlib.blake2b(a.data, digest_size=16).hexdigest()
+    return (a.shape, a.dtype.str, h)
+
+
+def cached_filter_keys(positive_X, side, E, dev):
+    P = np.asarray(positive_X.cpu() if isinstance(positive_X, torch.Tensor) else positive_X)
+    key = (_fingerprint(P), side, int(E), str(dev))
+    hit = _FILTER_CACHE.pop(key, None)
+    if hit is None:
+        PX = torch.as_tensor(P, dtype=torch.int64).to(dev).reshape(-1, 3)
+        hit = filter_keys(PX, side, E)
+        while len(_FILTER_CACHE) >= _FILTER_CACHE_MAX:
+            _FILTER_CACHE.pop(next(iter(_FILTER_CACHE)))
+    _FILTER_CACHE[key] = hit     # most recent last
+    return hit
 
 
 # ---------------------------------------------------------------- entry
@@ -264,9 +311,8 @@ def batched_ranks(model, eval_X, corrupt_side, positive_X=None, flags=0):
     if groups is None:
         raise NotImplementedError("no batched ranking for this model / score")
     if positive_X is not None:
-        PX = torch.as_tensor(np.asarray(positive_X.cpu() if isinstance(positive_X, torch.Tensor) else positive_X),
-                             dtype=torch.int64).to(dev).reshape(-1, 3)
-        fb, fe, fent = filter_index(X, PX, corrupt_side, E)
+        fkeys, fent = cached_filter_keys(positive_X, corrupt_side, E, dev)
+        fb, fe = filter_lookup(X, fkeys, fent, corrupt_side, E)
     ranks = torch.zeros(n, dtype=torch.int64, device=dev)
     pos = torch.zeros(n, dtype=torch.float32, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)

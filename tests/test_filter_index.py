@@ -46,3 +46,24 @@ def test_filter_index_two_sort_path():
     X = P[:80].clone()
     for side in ("h", "t"):
         _check(X, P, E, side)
+
+
+def test_cached_filter_keys_follow_the_content():
+    """The cached pairs equal a fresh build; an in-place edit of the positive
+    set is a new key (content hash), not a stale hit."""
+    g = np.random.default_rng(2)
+    E, R = 40, 5
+    P = np.stack([g.integers(0, E, 300), g.integers(0, R, 300), g.integers(0, E, 300)], 1)
+    ranking._FILTER_CACHE.clear()
+    k1, e1 = ranking.cached_filter_keys(P, "t", E, "cpu")
+    k2, e2 = ranking.cached_filter_keys(P.copy(), "t", E, "cpu")
+    assert k1 is k2 and e1 is e2
+    fk, fe = ranking.filter_keys(torch.as_tensor(P), "t", E)
+    assert torch.equal(k1, fk) and torch.equal(e1, fe)
+    P[0] = [E - 1, R - 1, E - 1]
+    k3, e3 = ranking.cached_filter_keys(P, "t", E, "cpu")
+    fk, fe = ranking.filter_keys(torch.as_tensor(P), "t", E)
+    assert k3 is not k1 and torch.equal(k3, fk) and torch.equal(e3, fe)
+    for i in range(6):
+        ranking.cached_filter_keys(P[i:], "h", E, "cpu")
+    assert len(ranking._FILTER_CACHE) == ranking._FILTER_CACHE_MAX
