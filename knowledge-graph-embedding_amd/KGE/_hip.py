@@ -27,6 +27,7 @@ FLAG_PHASE_SCORE = 32
 FLAG_PHASE_UPDATE = 64
 FLAG_OWNER = 128
 FLAG_OWNER_MERGE = 256
+FLAG_DEBUG_NO_REL_SEG = 512   # test hook: relation rows in the update kernel (compact launches)
 RANK_TRANS, RANK_ROT, RANK_MUL, RANK_DOT = range(4)
 RANK_FLAG_LANE_PASS = 1
 RPROJ_NONE, RPROJ_HYPER, RPROJ_RANK1 = range(3)

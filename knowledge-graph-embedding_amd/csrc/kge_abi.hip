@@ -357,6 +357,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.p = d->score_p;
   A.rel_reg = (model == KGE_MODEL_DISTMULT && d->constraint) ? d->constraint_weight : 0.f;
   A.rel_dests = !rescal;
+  // compact launches of the element-wise family: relation rows by rel_seg_kernel
+  A.rel_seg = compact && !rescal && !transr && !proj && !own && !(d->flags & KGE_FLAG_DEBUG_NO_REL_SEG);
   A.dense = rescal && A.train;
   A.dense_ent = rescal ? (float)(2.0 * d->constraint_weight / (double)E) : 0.f;
   A.lr = d->lr;
@@ -411,7 +413,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     A.own_planes = d->corrupt_side == KGE_SIDE_HT ? 2 : 1;
     A.own_rows_from = d->owner_rows_from;
     A.own_rec = d->owner_records;
-    A.rec_cols = kRecHead + 3 * FL;
+    A.rec_cols = kRecHead + (model == KGE_MODEL_TRANSE && P.sk != SK_DOT ? 2 : 3) * FL;   // rec_img<M>
     A.own_stats = d->owner_stats;
     A.own_stats_out = d->owner_stats_out;
     A.own_cap = (uint32_t)(own ? T : 0);
@@ -669,7 +671,8 @@ uint32_t kge_step_plan_signature(const kge_step_desc* d) {
 int64_t kge_owner_record_floats(const kge_step_desc* d) {
   Plan P;
   if (make_plan(d, &P) != KGE_OK) return 0;
-  return P.A.rec_cols > 0 ? P.A.rec_cols : kRecHead + 3 * 64 * P.G.vec * P.G.nc;
+  return P.A.rec_cols > 0 ? P.A.rec_cols
+                         : kRecHead + (d->model == KGE_MODEL_TRANSE && P.sk != SK_DOT ? 2 : 3) * 64 * P.G.vec * P.G.nc;
 }
 
 kge_status kge_step(const kge_step_desc* d, void* stream) {

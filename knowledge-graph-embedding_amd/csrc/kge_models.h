@@ -236,6 +236,11 @@ struct TransE {
   static constexpr bool CPLX = false;
   static constexpr bool WIDE = false;   // score kernel fits 128 VGPRs at one chunk (4 waves / SIMD)
   static constexpr bool SELF_CTX = false;   // context rows computed by the score kernel itself (RESCAL)
+  // owner-side scoring records carry the h and t accumulators only: an Lp
+  // score is a function of h + r - t, so d/dr = d/dh for a t-corrupt slot and
+  // -d/dt for an h-corrupt one -- the r accumulator is h - t (finish below);
+  // Dot keeps all three
+  static constexpr int REC_IMG = SK == SK_DOT ? 3 : 2;
   static constexpr bool FAST_STREAM = false;   // stream partial / gradient in hardware-rate forms (RotatE)
   static constexpr bool MAT = false;   // negatives' entity gradients re-derived, not materialised
   static constexpr int NSNAP = 2;

@@ -123,16 +123,25 @@ __global__ __launch_bounds__(kMergeWaves * KGE_WAVE) void owner_merge_kernel(Ste
 #pragma unroll
       for (int v = 0; v < 4; ++v) n[v] += fo * fo * h[4 + v];
       if (A.train) {
-        F x;
+        F x, y;
         load_row(x, h + kRecHead, FL);
 #pragma unroll
         for (int q = 0; q < VEC * NC; ++q) gH.v[q] += fo * x.v[q];
-        load_row(x, h + kRecHead + FL, FL);
+        if constexpr (rec_img<M>::n == 2) {   // r accumulator = h - t (TransE, kge_models.h)
+          load_row(y, h + kRecHead + FL, FL);
 #pragma unroll
-        for (int q = 0; q < VEC * NC; ++q) gR.v[q] += fo * x.v[q];
-        load_row(x, h + kRecHead + 2 * FL, FL);
+          for (int q = 0; q < VEC * NC; ++q) {
+            gR.v[q] += fo * (x.v[q] - y.v[q]);
+            gT.v[q] += fo * y.v[q];
+          }
+        } else {
+          load_row(y, h + kRecHead + FL, FL);
 #pragma unroll
-        for (int q = 0; q < VEC * NC; ++q) gT.v[q] += fo * x.v[q];
+          for (int q = 0; q < VEC * NC; ++q) gR.v[q] += fo * y.v[q];
+          load_row(y, h + kRecHead + 2 * FL, FL);
+#pragma unroll
+          for (int q = 0; q < VEC * NC; ++q) gT.v[q] += fo * y.v[q];
+        }
       }
     }
     float rsq = 0.f;

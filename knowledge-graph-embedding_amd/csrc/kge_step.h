@@ -1,5 +1,6 @@
 // Kernel-argument structs shared by the step kernels and the C-ABI layer.
 #pragma once
+#include <type_traits>
 
 #include "kge_models.h"
 
@@ -163,6 +164,12 @@ struct StepArgs {
   // main pass; scale[] slots of the pass's entity / relation variable
   bool keep_cnt = false;
   bool rel_only = false;   // visit the relation destinations only (TransH rel_hyper pass)
+  // compact launches: the relation rows are summed by rel_seg_kernel (a
+  // workgroup per relation, the positives' rows in ascending order, 32 in
+  // flight) instead of by one update wave per relation -- a Zipf-hot
+  // relation's list (~300 keys at C5) was a 100 us serial chain there; the
+  // update kernel only empties their list slots
+  bool rel_seg = false;
   // entity ids -> table rows: n_ent global ids; rG > 1: the table is G
   // all-gathered shards of rEs rows, id e at (e mod rG) * rEs + e div rG
   int64_t n_ent = 0;
@@ -226,6 +233,10 @@ struct StepArgs {
   float* own_err = nullptr;         // owner: set to 1 when the owned keys exceed own_cap
   bool own_keys = false;            // update kernel: compact key positions [0, ctl->own_len)
 };
+// accumulator images per owner record: M::REC_IMG when the model declares it
+// (TransE: h, t), else 3 (h, r, t)
+template <class M, class = void> struct rec_img { static constexpr int n = 3; };
+template <class M> struct rec_img<M, std::void_t<decltype(M::REC_IMG)>> { static constexpr int n = M::REC_IMG; };
 constexpr int kRecHead = 16;        // owner record: Ms, Z, loss part, hinge / logistic weight, norm^2 x4, -
 
 struct StepGeom {

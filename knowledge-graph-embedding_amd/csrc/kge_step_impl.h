@@ -810,12 +810,14 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   // ---- the positives' row gradients: sum of the waves' scaled accumulators
   if constexpr (OWN) {
     if (A.train) {   // the record's accumulator images (merged at the owner's maximum)
-      for (int e = tid; e < nValid * 3 * FL; e += blockDim.x) {
-        const int p = e / (3 * FL), rem = e % (3 * FL);
+      constexpr int NI = rec_img<M>::n;   // 2: h and t (image v -> accumulator 2v), 3: h, r, t
+      for (int e = tid; e < nValid * NI * FL; e += blockDim.x) {
+        const int p = e / (NI * FL), rem = e % (NI * FL);
         const int v = rem / FL, k = rem % FL;
+        const int src = NI == 2 ? 2 * v : v;
         const float* mg = s_mrg + p * MG_STRIDE;
         float sum = 0.f;
-        for (int g = 0; g < wpp; ++g) sum += mg[MG_F + g] * red[((p * wpp + g) * 3 + v) * FL + k];
+        for (int g = 0; g < wpp; ++g) sum += mg[MG_F + g] * red[((p * wpp + g) * 3 + src) * FL + k];
         A.own_rec[(i0 + p) * (int64_t)A.rec_cols + kRecHead + v * FL + k] = sum;
       }
     }
@@ -1480,7 +1482,7 @@ void update_kernel(StepArgs A) {
       constexpr int r = decltype(rc)::value;
       act[r] = ws_ok && dd * KR + r < nkeys && t[r].y != 0xFFFFFFFFu &&
                !(A.rel_only && (int64_t)t[r].x < E_);
-      if (abort_) {   // (the leader's slot: one per destination)
+      if (abort_ || (A.rel_seg && (int64_t)t[r].x >= E_)) {   // (the leader's slot: one per destination)
         if (act[r] && lane == 0 && !A.keep_cnt) A.htab[t[r].z] = 0ull;
         act[r] = false;
       }
@@ -1538,8 +1540,9 @@ void update_kernel(StepArgs A) {
   } else {
     const bool active = ws_ok && dd < (A.rel_only ? R_ : ndest);
     const int64_t d = dd < R_ ? E_ + dd : dd - R_;
-    if (abort_ && active && lane == 0 && !A.keep_cnt) A.cnt[d] = 0u;
-    run_dest(d, d, 0xFFFFFFFFu, active && !abort_);
+    const bool skip = abort_ || (A.rel_seg && d >= E_);
+    if (skip && active && lane == 0 && !A.keep_cnt) A.cnt[d] = 0u;
+    run_dest(d, d, 0xFFFFFFFFu, active && !skip);
   }
   if (A.dense) {
     // ||dense gradient||^2: workgroup partial; partials_norm_kernel (the next
@@ -1560,6 +1563,91 @@ void update_kernel(StepArgs A) {
     }
   }
   KGE_PROF(16);
+}
+
+// ------------------------------------------------------------ relation rows
+// (A.rel_seg) One workgroup per (relation r, 256-column strip). The batch's
+// relation ids are scanned kRsChunk at a time -- every id load of a chunk in
+// flight together, coalesced (id base + k 256 + tid) -- and the positives of
+// r listed in LDS in ascending order (a ballot per (k, wave), their counts
+// prefix-summed in that order). Each thread then sums its column of those
+// positives' relation-row gradients (gpos) in list order, kRsU rows in
+// flight: the order, and so the bits, of the update kernel's ascending-code
+// sum (a Zipf-hot relation's ~300 rows take a handful of round trips instead
+// of one per two rows). Then the update kernel's relation write: the raw
+// gradient (grad / split update modes) or the clip-scaled SGD step;
+// relations with no positive are left alone (grad mode with zero_untouched:
+// a zero row). Flat rows: both fragment layouts (load_row, load_row_half)
+// keep element e at float e.
+constexpr int kRsThreads = 256, kRsK = 8, kRsChunk = kRsK * kRsThreads, kRsU = 48;
+
+template <int UNUSED>
+__global__ __launch_bounds__(kRsThreads) void rel_seg_kernel(StepArgs A) {
+  constexpr int NW = kRsThreads / KGE_WAVE;
+  __shared__ int32_t s_list[kRsChunk];
+  __shared__ int32_t s_wcnt[kRsK * NW];
+  if (ws_refused(A.ctl, A.sig, A.status, nullptr)) return;
+  if (A.abort_flag && *A.abort_flag != 0.f) return;
+  const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const int64_t r = blockIdx.x;
+  const int cols = A.rel.cols;
+  const int c = (int)blockIdx.y * kRsThreads + tid;
+  const bool cv = c < cols;
+  const float* g = A.gpos + A.gcols + (cv ? c : 0);
+  const int64_t gstride = 3 * (int64_t)A.gcols;
+  float acc = 0.f;
+  int64_t tot = 0;
+  for (int64_t base = 0; base < A.B; base += kRsChunk) {
+    int64_t rid[kRsK];
+#pragma unroll
+    for (int k = 0; k < kRsK; ++k) {
+      const int64_t i = base + k * kRsThreads + tid;
+      rid[k] = i < A.B ? load_idx(A.pos, i * 3 + 1, A.i64) : -1;
+    }
+    uint64_t m[kRsK];
+#pragma unroll
+    for (int k = 0; k < kRsK; ++k) {
+      m[k] = __ballot(rid[k] == r);
+      if (lane == 0) s_wcnt[k * NW + wv] = __popcll(m[k]);
+    }
+    __syncthreads();
+    int n = 0;
+#pragma unroll
+    for (int k = 0; k < kRsK; ++k) {
+      int off = n;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        if (w < wv) off += s_wcnt[k * NW + w];
+        n += s_wcnt[k * NW + w];
+      }
+      if (rid[k] == r) s_list[off + __popcll(m[k] & ((1ull << lane) - 1ull))] = k * kRsThreads + tid;
+    }
+    __syncthreads();
+    for (int p0 = 0; p0 < n; p0 += kRsU) {
+      float x[kRsU];
+#pragma unroll
+      for (int u = 0; u < kRsU; ++u) x[u] = cv ? g[(base + s_list[min(p0 + u, n - 1)]) * gstride] : 0.f;
+#pragma unroll
+      for (int u = 0; u < kRsU; ++u)
+        if (p0 + u < n) acc += x[u];
+    }
+    tot += n;
+    __syncthreads();   // s_list / s_wcnt are rewritten by the next chunk
+  }
+  if (!cv) return;
+  if (A.grad_mode || A.rel_grad) {
+    if (tot > 0 || A.zero_untouched) A.grel[r * (int64_t)A.rel_gcols + c] = acc;
+  } else if (tot > 0) {
+    float sc = A.ctl->scale[A.sc_rel_idx];
+    if (A.scale_from_norm2) sc = -A.lr * (A.clip_norm / fmaxf(sqrtf(A.norm2_out[A.sc_rel_idx]), A.clip_norm));
+    float* w = A.rel.row_w(r) + c;
+    *w = *w + acc * sc;
+  }
+}
+
+static inline void launch_rel_seg(const StepArgs& A, hipStream_t st) {
+  const dim3 grid((unsigned)A.rel.rows, (unsigned)((A.rel.cols + kRsThreads - 1) / kRsThreads));
+  hipLaunchKernelGGL(rel_seg_kernel<0>, grid, dim3(kRsThreads), 0, st, A);
 }
 
 // ------------------------------------------------------------ dispatch
@@ -1592,9 +1680,10 @@ static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_
                            dim3(kUpdThreads), 0, st, A);
       else
         hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK, 1, true>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
-      return KGE_OK;
+    } else {
+      hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
     }
-    hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
+    if (A.rel_seg) launch_rel_seg(A, st);
   }
   return KGE_OK;
 }

@@ -1149,3 +1149,26 @@ def test_sharded_step_c5_shard_size(hiplib, loopback):
         assert float((outs[0][2] - outs[1][2]).abs().max()) <= 1e-5
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("model_name", ["TransE", "DistMult", "RotatE"])
+def test_rel_seg_hot_relation(hiplib, model_name):
+    """Compact launch with a Zipf-hot relation: 3000 positives (past one 2048-id
+    scan chunk of rel_seg_kernel), 70 % of them on relation 0. The relation rows
+    summed by the per-relation segment pass equal the oracle, and equal the
+    update kernel's own relation path (KGE_FLAG_DEBUG_NO_REL_SEG) bit for bit."""
+    from KGE import _hip, loss, score
+    E, R, B = 100000, 6, 3000
+    rng = np.random.default_rng(21)
+    rel = np.where(rng.random(B) < 0.7, 0, rng.integers(1, R, B))
+    pos = np.stack([rng.integers(0, E, B), rel, rng.integers(0, E, B)], 1).astype(np.int64)
+    sc = None if model_name == "DistMult" else score.LpDistance(2)
+    outs = []
+    for flags in (0, _hip.FLAG_DEBUG_NO_REL_SEG):
+        ref, got, l_, ps, ns, step, _ = run_case(hiplib, model_name, 32, B, 4, "h+t", sc,
+                                                 loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E=E, R=R,
+                                                 constraint=False, pos=pos, flags=flags, seed=5)
+        check(ref, got, l_, ps, ns)
+        outs.append(got)
+    for k in outs[0]:
+        assert np.array_equal(outs[0][k], outs[1][k]), k

@@ -18,9 +18,15 @@ KERNELS = ("score_kernel", "update_kernel", "constrain_rows_kernel", "apply_kern
 
 
 def short(name):
+    """kge kernels by their short name (templates folded); others dropped."""
     for k in KERNELS:
         if k in name:
             return k
+    if "kge::" in name:
+        base = name.split("kge::", 1)[1]
+        for sep in ("<", "("):
+            base = base.split(sep, 1)[0]
+        return base
     return None
 
 
