@@ -170,9 +170,10 @@ enum {
    *       update pass (remote_rows_from, relation gradients to grad_out[1]). */
   KGE_FLAG_OWNER = 128,
   KGE_FLAG_OWNER_MERGE = 256,
-  KGE_FLAG_DEBUG_NO_REL_SEG = 512   /* test hook: compact launches sum the relation rows in
-                                       the update kernel (one wave per relation) instead of
-                                       the per-relation segment pass; same order, same bits */
+  KGE_FLAG_DEBUG_NO_REL_SEG = 512   /* test hook: the owner merge's update pass sums the
+                                       relation rows in the update kernel (one wave per
+                                       relation) instead of the per-relation segment pass;
+                                       same order, same bits */
 };
 
 typedef struct kge_table {

@@ -331,6 +331,7 @@ class FusedStep:
             if neg_score is not None:
                 d.neg_score_out = neg_score.data_ptr()
             if sig != self._ws_sig:   # another cached plan ran in between
+                self._refuse_split_wipe(d)
                 self.workspace.zero_()
                 self._ws_sig = sig
         else:
@@ -347,6 +348,7 @@ class FusedStep:
             elif sig != self._ws_sig:
                 # a different plan lays the workspace out differently (the
                 # library would refuse the stamped buffer): zeros again
+                self._refuse_split_wipe(d)
                 self.workspace.zero_()
             self._ws_sig = sig
             d.workspace = self.workspace.data_ptr()
@@ -355,6 +357,15 @@ class FusedStep:
                 self._descs.clear()
             self._descs[key] = (d, sig)   # (the split step alternates two descriptors)
         return d
+
+    def _refuse_split_wipe(self, d):
+        """A PHASE_UPDATE call consumes the lists its PHASE_SCORE call left in
+        the workspace; a plan change in between (any descriptor field in the
+        signature, flags included) would zero them and make the update a
+        silent no-op."""
+        if (d.flags & _hip.FLAG_PHASE_UPDATE) and self._ws_sig is not None:
+            raise RuntimeError("split step: the PHASE_UPDATE descriptor's plan differs from its PHASE_SCORE "
+                               "call's (every field but the phase flags must match)")
 
     def bind(self, batch, is_train, optimizer, accum=None):
         """A callable running this step again and again on ``batch``'s buffer

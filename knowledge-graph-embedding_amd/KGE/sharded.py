@@ -158,6 +158,7 @@ class ShardedStep:
         if mode == "owner" and self.mid not in _SPLIT:
             raise NotImplementedError("owner-side scoring covers TransE, DistMult and RotatE")
         self.mode = mode
+        self.debug_flags = 0   # test hooks (KGE_FLAG_DEBUG_*) for the owner merge's update pass
         self.loopback = bool(loopback)
         self.slack = float(capacity_slack)
         self.cap_floor = int(capacity_floor)
@@ -895,7 +896,7 @@ class ShardedStep:
         # 4. records to the positives' ranks; 5. merge
         if G > 1:
             ex.all_to_all(o["rec_in"], o["rec"])
-        fm.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER_MERGE | _hip.FLAG_PHASE_SCORE
+        fm.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER_MERGE | _hip.FLAG_PHASE_SCORE | self.debug_flags
         fm(lpos, is_train, opt)
         # 6. [norm^2 x4 | loss | - | - | error flag], the stats
         small = self.red[-8:]
@@ -910,7 +911,7 @@ class ShardedStep:
         fo.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER | _hip.FLAG_PHASE_UPDATE
         fo.abort = small[-1:]
         fo(o["gtrip"], True, optimizer, neg_ids=o["gneg"], prof_events=ev_u)
-        fm.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER_MERGE | _hip.FLAG_PHASE_UPDATE
+        fm.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER_MERGE | _hip.FLAG_PHASE_UPDATE | self.debug_flags
         fm.abort = small[-1:]
         fm(lpos, True, optimizer)
         # 9. relation gradients; the fetched rows' gradients back to their owners

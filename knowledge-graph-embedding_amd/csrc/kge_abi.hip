@@ -49,11 +49,12 @@ struct Plan {
   // dense-gradient / relation-matrix models (RESCAL)
   uint64_t o_upart, o_sorted, o_srel, o_gproj, o_rpart, o_regpart, o_gent, o_grel;
   uint64_t o_gneg, o_dm;   // TransR
-  uint64_t o_leaders, o_htab, o_relseg;
+  uint64_t o_leaders, o_htab, o_relseg, o_lng;
   int hbits;
   uint64_t o_gnegp, o_gpos2, o_gdense[3], o_dpart;   // TransH / TransD
   uint64_t o_owncodes;                               // owner-side scoring
-  bool rescal, transr, proj, td, pj_dense, own, omerge;
+  bool rescal, transr, proj, td, pj_dense, own, omerge, pos_only;
+  uint32_t lng_cap;
   uint32_t sig;   // workspace plan signature
 };
 
@@ -357,8 +358,10 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   A.p = d->score_p;
   A.rel_reg = (model == KGE_MODEL_DISTMULT && d->constraint) ? d->constraint_weight : 0.f;
   A.rel_dests = !rescal;
-  // compact launches of the element-wise family: relation rows by rel_seg_kernel
-  A.rel_seg = compact && !rescal && !transr && !proj && !own && !(d->flags & KGE_FLAG_DEBUG_NO_REL_SEG);
+  // the owner merge's update pass (compact): relation rows by rel_seg_kernel.
+  // Not in the other compact launches: there the update kernel's hot-relation
+  // waves overlap its ~10^5 other waves, and the extra launch cost C5 24 us
+  A.rel_seg = compact && omerge && !(d->flags & KGE_FLAG_DEBUG_NO_REL_SEG);
   A.dense = rescal && A.train;
   A.dense_ent = rescal ? (float)(2.0 * d->constraint_weight / (double)E) : 0.f;
   A.lr = d->lr;
@@ -471,6 +474,12 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     }
   }
   if (own) P.o_owncodes = take((uint64_t)T * 4);
+  // owner merge, SGD update pass: long destination lists deferred (kLongN)
+  const bool pos_only = omerge && compact && d->optimizer == KGE_OPT_SGD && !fuse_norm_plan && entc <= 256 * kLongCPT;
+  const uint32_t lng_cap = (uint32_t)(T / kLongN + 1);
+  if (pos_only) P.o_lng = take((uint64_t)lng_cap * 16);
+  P.pos_only = pos_only;
+  P.lng_cap = lng_cap;
   P.ws_bytes = std::max<uint64_t>(off, 256);
   // the plan's workspace signature (kge_hip.h): FNV-1a over everything that
   // decides where a counter, list or ticket lives and what it means
@@ -702,6 +711,11 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   A.gpe_stride = 3 * A.gcols;
   A.gpe_toff = 2 * A.gcols;
   if (P.own) A.own_codes = (uint32_t*)(ws + P.o_owncodes);
+  if (P.pos_only) {
+    A.pos_only = true;
+    A.lng = (uint4*)(ws + P.o_lng);
+    A.lng_cap = P.lng_cap;
+  }
   if (P.own || P.omerge) {
     // owner-side scoring: OWNER | SCORE (owner pass), OWNER | UPDATE
     // (coefficients + the owned rows' update), OWNER_MERGE | SCORE (merge),

@@ -29,6 +29,9 @@ constexpr int kMaxWpp = kStepWaves > 8 ? kStepWaves : 8;   // waves per positive
 #endif
 constexpr int kMergeStride = kMaxWpp + 24;   // floats of per-positive merge state in the score kernel's LDS
 constexpr int kSortMax = 1024;     // update kernel: longest destination list sorted in LDS (per wave)
+// owner merge update: destinations with more than kLongN (and at most
+// kLongMax) keys go to long_rows_kernel (kLongWGs workgroups, kLongU rows in flight)
+constexpr int kLongN = 64, kLongMax = 4096, kLongWGs = 64, kLongU = 32, kLongCPT = 4;   // (rows <= 1024 floats)
 
 // Control block at the head of the workspace. The caller zero-fills the
 // workspace once when it allocates it; every kernel that uses a word puts it
@@ -48,7 +51,8 @@ struct StepCtl {
   uint32_t pad1;
   uint32_t own_count;      // owner score pass: key positions taken (per-workgroup blocks)
   uint32_t own_len;        // ... handed to the coefficient / update passes by the last workgroup
-  uint32_t pad2[2];
+  uint32_t lng_count;      // merge update: long destinations deferred to long_rows_kernel (reset by the merge)
+  uint32_t pad2;
 };
 
 // Workspace plan guard (include/kge_hip.h, "workspace"). Every kernel of a
@@ -164,12 +168,19 @@ struct StepArgs {
   // main pass; scale[] slots of the pass's entity / relation variable
   bool keep_cnt = false;
   bool rel_only = false;   // visit the relation destinations only (TransH rel_hyper pass)
-  // compact launches: the relation rows are summed by rel_seg_kernel (a
-  // workgroup per relation, the positives' rows in ascending order, 32 in
-  // flight) instead of by one update wave per relation -- a Zipf-hot
-  // relation's list (~300 keys at C5) was a 100 us serial chain there; the
-  // update kernel only empties their list slots
+  // owner merge update (compact): the relation rows are summed by
+  // rel_seg_kernel (a workgroup per relation, the positives' rows in
+  // ascending order) instead of by one update wave per relation -- a
+  // Zipf-hot relation's list (~250 keys at C5) was a serial chain there that
+  // nothing else overlapped; the update kernel only empties their list slots
   bool rel_seg = false;
+  // merge update (KGE_FLAG_OWNER_MERGE | PHASE_UPDATE, SGD): every key is a
+  // positive's own row gradient; a destination with more than kLongN of them
+  // (a Zipf-hot head or tail) is handed to long_rows_kernel (lng[], up to
+  // lng_cap) instead of being summed by one wave two rows at a time
+  bool pos_only = false;
+  uint4* lng = nullptr;
+  uint32_t lng_cap = 0;
   // entity ids -> table rows: n_ent global ids; rG > 1: the table is G
   // all-gathered shards of rEs rows, id e at (e mod rG) * rEs + e div rG
   int64_t n_ent = 0;

@@ -802,7 +802,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
     for (int v = 0; v < 4; ++v) mg[MG_N + v] = n[v];
     mg[MG_MS] = Ms;
     mg[MG_IZ] = invZ;
-    if (A.pos_score_out) A.pos_score_out[i0 + p] = spv;
+    if (A.pos_score_out) A.pos_score_out[(i0 + p)] = spv;
   }
   __syncthreads();
   KGE_PROF(3);
@@ -1195,6 +1195,19 @@ void update_kernel(StepArgs A) {
     // issued together: the counter, the list's first 64 entries (speculative;
     // lanes past the count are ignored) and the entity row
     const uint32_t n = CMP ? (uint32_t)A.htab[li] : A.cnt[d];
+    if constexpr (CMP) {
+      // merge update, a long list: long_rows_kernel takes it (all threads of a
+      // workgroup, kLongU rows in flight) if there is room in lng[]
+      if (A.pos_only && is_ent && n > (uint32_t)kLongN && n <= (uint32_t)kLongMax) {
+        uint32_t slot = 0u;
+        if (lane == 0) slot = atomicAdd(&A.ctl->lng_count, 1u);
+        slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)slot);
+        if (slot < A.lng_cap) {
+          if (lane == 0) A.lng[slot] = make_uint4((uint32_t)d, (uint32_t)((uint64_t)d >> 32), (uint32_t)li, code1);
+          return;
+        }
+      }
+    }
     // list entry q (compact launches: position 0 is the leader's code1, and
     // the list is read only once the count says there is more than one key)
     const bool l0 = KGE_COMPACT_LIST0 && CMP;
@@ -1565,6 +1578,93 @@ void update_kernel(StepArgs A) {
   KGE_PROF(16);
 }
 
+// ------------------------------------------------------------ long lists
+// (A.pos_only, the owner merge's update pass) One destination row per
+// workgroup iteration: its codes -- list position 0 from the leader, the
+// list, then its overflow entries -- gathered into LDS and bitonic-sorted,
+// each thread summing one column of the positives' row gradients (gpe) in
+// ascending code order with kLongU rows in flight (the update kernel's
+// order: the same bits), then the update kernel's write (raw gradient for a
+// fetched row, else the clip-scaled SGD step) and the hash slot emptied.
+template <int UNUSED>
+__global__ __launch_bounds__(256) void long_rows_kernel(StepArgs A) {
+  __shared__ uint32_t s_codes[kLongMax];
+  __shared__ uint32_t s_fill;
+  if (ws_refused(A.ctl, A.sig, A.status, nullptr)) return;
+  const int tid = threadIdx.x;
+  const uint32_t nitems = min(A.ctl->lng_count, A.lng_cap);
+  float sc = A.ctl->scale[A.sc_ent_idx];
+  if (A.scale_from_norm2) sc = -A.lr * (A.clip_norm / fmaxf(sqrtf(A.norm2_out[A.sc_ent_idx]), A.clip_norm));
+  const uint32_t nneg = A.nkeyneg;
+  for (uint32_t it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const uint4 w = A.lng[it];
+    const int64_t d = (int64_t)((uint64_t)w.x | ((uint64_t)w.y << 32));
+    const int64_t li = w.z;
+    const uint32_t n = (uint32_t)A.htab[li];
+    const uint32_t nl = min(n, (uint32_t)A.cap);
+    const uint32_t* lst = A.list + li * (int64_t)A.cap;
+    for (uint32_t q = tid; q < nl; q += 256) s_codes[q] = (KGE_COMPACT_LIST0 && q == 0u) ? w.w : lst[q];
+    if (tid == 0) s_fill = nl;
+    __syncthreads();
+    if (n > nl) {
+      const uint32_t novf = A.ctl->ovf_len;
+      for (uint32_t q = tid; q < novf; q += 256) {
+        const uint64_t y = A.ovf[q];
+        if ((int64_t)(y >> 32) == d) s_codes[atomicAdd(&s_fill, 1u)] = (uint32_t)y;
+      }
+    }
+    uint32_t P = 1;
+    while (P < n) P <<= 1;
+    for (uint32_t q = n + tid; q < P; q += 256) s_codes[q] = 0xFFFFFFFFu;
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t i = tid; i < P; i += 256) {
+          const uint32_t l = i ^ j;
+          if (l > i) {
+            const uint32_t a = s_codes[i], b = s_codes[l];
+            if ((a > b) == ((i & k) == 0)) { s_codes[i] = b; s_codes[l] = a; }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // every column of this thread (kLongCPT of them) in each batch of rows
+    float acc[kLongCPT];
+#pragma unroll
+    for (int j = 0; j < kLongCPT; ++j) acc[j] = 0.f;
+    for (uint32_t p0 = 0; p0 < n; p0 += kLongU) {
+      float x[kLongU][kLongCPT];
+#pragma unroll
+      for (int u = 0; u < kLongU; ++u) {
+        const uint32_t code = s_codes[min(p0 + (uint32_t)u, n - 1u)] - nneg;   // (positive codes only)
+        const float* g = A.gpe + (int64_t)(code >> 2) * A.gpe_stride + ((code & 3u) == 0u ? 0 : A.gpe_toff);
+#pragma unroll
+        for (int j = 0; j < kLongCPT; ++j) {
+          const int c = tid + 256 * j;
+          x[u][j] = c < A.ent.cols ? g[c] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kLongU; ++u)
+        if (p0 + (uint32_t)u < n) {
+#pragma unroll
+          for (int j = 0; j < kLongCPT; ++j) acc[j] += x[u][j];
+        }
+    }
+    float* row = A.ent.row_w(d);
+#pragma unroll
+    for (int j = 0; j < kLongCPT; ++j) {
+      const int c = tid + 256 * j;
+      if (c >= A.ent.cols) continue;
+      if (d >= A.remote_from) row[c] = acc[j];
+      else row[c] = row[c] + acc[j] * sc;
+    }
+    if (tid == 0 && !A.keep_cnt) A.htab[li] = 0ull;
+    __syncthreads();   // s_codes is rewritten by the next destination
+  }
+}
+
 // ------------------------------------------------------------ relation rows
 // (A.rel_seg) One workgroup per (relation r, 256-column strip). The batch's
 // relation ids are scanned kRsChunk at a time -- every id load of a chunk in
@@ -1684,6 +1784,7 @@ static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_
       hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
     }
     if (A.rel_seg) launch_rel_seg(A, st);
+    if (A.pos_only) hipLaunchKernelGGL(long_rows_kernel<0>, dim3(kLongWGs), dim3(256), 0, st, A);
   }
   return KGE_OK;
 }

@@ -1152,23 +1152,70 @@ def test_sharded_step_c5_shard_size(hiplib, loopback):
 
 
 @pytest.mark.parametrize("model_name", ["TransE", "DistMult", "RotatE"])
-def test_rel_seg_hot_relation(hiplib, model_name):
-    """Compact launch with a Zipf-hot relation: 3000 positives (past one 2048-id
-    scan chunk of rel_seg_kernel), 70 % of them on relation 0. The relation rows
-    summed by the per-relation segment pass equal the oracle, and equal the
-    update kernel's own relation path (KGE_FLAG_DEBUG_NO_REL_SEG) bit for bit."""
-    from KGE import _hip, loss, score
+def test_compact_hot_relation(hiplib, model_name):
+    """Compact launch with a Zipf-hot relation: 3000 positives, 70 % of them on
+    relation 0 (a relation list far past its capacity, sorted in LDS) == the
+    oracle."""
+    from KGE import loss, score
     E, R, B = 100000, 6, 3000
     rng = np.random.default_rng(21)
     rel = np.where(rng.random(B) < 0.7, 0, rng.integers(1, R, B))
     pos = np.stack([rng.integers(0, E, B), rel, rng.integers(0, E, B)], 1).astype(np.int64)
     sc = None if model_name == "DistMult" else score.LpDistance(2)
-    outs = []
-    for flags in (0, _hip.FLAG_DEBUG_NO_REL_SEG):
-        ref, got, l_, ps, ns, step, _ = run_case(hiplib, model_name, 32, B, 4, "h+t", sc,
-                                                 loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E=E, R=R,
-                                                 constraint=False, pos=pos, flags=flags, seed=5)
-        check(ref, got, l_, ps, ns)
-        outs.append(got)
-    for k in outs[0]:
-        assert np.array_equal(outs[0][k], outs[1][k]), k
+    ref, got, l_, ps, ns, step, _ = run_case(hiplib, model_name, 32, B, 4, "h+t", sc,
+                                             loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E=E, R=R,
+                                             constraint=False, pos=pos, seed=5)
+    check(ref, got, l_, ps, ns)
+
+
+@pytest.mark.parametrize("loopback", [False, True])
+def test_owner_merge_hot_entities(hiplib, loopback):
+    """Owner mode (world size 1, RCCL) on a table large enough for compact
+    launches, with Zipf-like hot rows among the positives: 40 % of the heads
+    are entity 7, 30 % of the tails entity 11, 60 % of the relations 0. The
+    merge's update pass hands the long destinations to long_rows_kernel and
+    the relation rows to rel_seg_kernel; two steps == two oracle steps, and
+    == (bit for bit) the same steps with the relation rows summed by the
+    update kernel itself (KGE_FLAG_DEBUG_NO_REL_SEG)."""
+    import torch.distributed as dist
+    from KGE import _hip, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    from KGE.sharded import ShardedStep
+    dev = _dev()
+    _init_world1(dist, dev)
+    try:
+        E, R, d, B, K = 100000, 6, 24, 400, 8
+        W = _weights("TransE", E, R, d, np.random.default_rng(17))
+        outs = []
+        for flags in (0, _hip.FLAG_DEBUG_NO_REL_SEG):
+            rng = np.random.default_rng(18)
+            m = _make("TransE", d, K, "h+t", score.LpDistance(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
+                      E, R, UniformStrategy(np.arange(E), seed=4), constraint=False)
+            m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
+            st = ShardedStep(m, mode="owner", loopback=loopback, local_fast=False)   # (not the one-rank shortcut)
+            st.debug_flags = flags
+            ref_w = W
+            opt = optimizers.SGD(0.05)
+            for it in range(2):
+                h = np.where(rng.random(B) < 0.4, 7, rng.integers(0, E, B))
+                t = np.where(rng.random(B) < 0.3, 11, rng.integers(0, E, B))
+                r = np.where(rng.random(B) < 0.6, 0, rng.integers(0, R, B))
+                pos = np.stack([h, r, t], 1).astype(np.int64)
+                plane = m.ns_strategy.offset
+                lv = float(st(torch.tensor(pos, device=dev), True, opt))
+                torch.cuda.synchronize()
+                st.check_status()
+                neg = orc.negatives(pos, K, "h+t", E, seed=4, plane=plane)
+                ref = orc.train_step("TransE", ref_w, pos, neg, score=("lp", 2.0), loss=("sans", 3.0, 1.0), lr=0.05,
+                                     constraint=False)
+                ref_w = ref["weights"]
+                assert abs(lv - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"])), it
+            st.sync()
+            for kk, v in ref_w.items():
+                np.testing.assert_allclose(m.model_weights[kk].cpu().numpy(), v, atol=TOL, err_msg=kk)
+            outs.append({kk: v.cpu().numpy() for kk, v in m.model_weights.items()})
+            del st
+        for kk in outs[0]:
+            assert np.array_equal(outs[0][kk], outs[1][kk]), kk
+    finally:
+        dist.destroy_process_group()
