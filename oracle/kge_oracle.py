@@ -300,6 +300,39 @@ def _score_hrt(model, W, L, h, r, t, score, cfg):
     raise ValueError(model)
 
 
+def filtered_ranks(model, weights, X, side, positive_X=None, score=("lp", 2.0), limit=None, constraint=False,
+                   tie_tol=1e-5):
+    """BaseModel.get_rank (BaseModel.py:620-654) for every triple of X, in
+    float64: every entity scored on the corrupted side (score_hrt with h or t
+    None), the known positives sharing the query's (r, kept entity) set to
+    -inf (:646-650), rank = 1 + #(scores > the true triple's score) (:652-654;
+    counted in int64, the reference's int16 overflows past 32,767).
+    Also returns, per query, the candidates within tie_tol * max(1, |s_true|)
+    of the true score: an fp32 evaluation may order those either way."""
+    W = {k: torch.tensor(np.asarray(v), dtype=F64) for k, v in weights.items()}
+    L = _Lookups(W, False)
+    cfg = {"constraint": constraint, "constraint_weight": 1.0, "limit": limit}
+    E = W["ent_emb"].shape[0]
+    X = np.asarray(X, dtype=np.int64).reshape(-1, 3)
+    P = None if positive_X is None else np.asarray(positive_X, dtype=np.int64).reshape(-1, 3)
+    keep, corr = (2, 0) if side == "h" else (0, 2)
+    every = np.arange(E)
+    ranks, ties = [], []
+    with torch.no_grad():
+        for x in X:
+            h = every if side == "h" else np.full(E, x[0])
+            t = every if side == "t" else np.full(E, x[2])
+            s = _score_hrt(model, W, L, h, np.full(E, x[1]), t, score, cfg).numpy().copy()
+            ps = float(_score_hrt(model, W, L, x[0:1], x[1:2], x[2:3], score, cfg).reshape(-1)[0])
+            near = int(np.sum(np.abs(s - ps) <= tie_tol * max(1.0, abs(ps))))
+            if P is not None:
+                m = (P[:, 1] == x[1]) & (P[:, keep] == x[keep])
+                s[P[m, corr]] = -np.inf
+            ranks.append(int(np.sum(s > ps)) + 1)
+            ties.append(near)
+    return np.array(ranks, dtype=np.int64), np.array(ties, dtype=np.int64)
+
+
 def _constraint(model, W, L, X, cfg, batch_scale):
     """Per-model _constraint_loss: assigns (no grad) + returned term."""
     if not cfg["constraint"]:

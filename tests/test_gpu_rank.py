@@ -150,3 +150,68 @@ def test_rank_tiled_pass_equals_lane_pass(name, si):
         tiled = ranking.batched_ranks(m, X, side, PX)
         lane = ranking.batched_ranks(m, X, side, PX, flags=_hip.RANK_FLAG_LANE_PASS)
         assert np.array_equal(tiled, lane), np.nonzero(tiled != lane)[0][:10]
+
+
+def _oracle_weights(m):
+    return {k: v.detach().cpu().numpy() for k, v in m.model_weights.items()}
+
+
+def _oracle_score(m):
+    from tests.test_gpu_step import _spec_score
+    sc = getattr(m, "score_fn", None)
+    return _spec_score(sc) if sc is not None else ("dot", 0.0)
+
+
+@pytest.mark.parametrize("name", MODELS)
+def test_rank_toy_matches_oracle(name, tmp_path):
+    """kge_rank vs the float64 restatement of get_rank in oracle/ (not the
+    package's own per-triple path): every model, both sides, unfiltered and
+    filtered by every known triple; ranks equal up to the oracle's near-ties."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import kge_oracle as orc
+    from KGE import ranking, score
+    train, val, md = toy()
+    sc = None if name in ("DistMult", "RESCAL") else (score.LpDistance(1) if name == "RotatE" else score.LpDistance(2))
+    m = build(name, sc)
+    m.train(train_X=train, val_X=val, metadata=md, epochs=2, batch_size=4, optimizer="SGD", seed=7,
+            log_path=str(tmp_path))
+    X = np.concatenate([train, val])
+    W = _oracle_weights(m)
+    for side in ("h", "t"):
+        for positive_X in (None, X):
+            got = ranking.batched_ranks(m, X, side, positive_X)
+            ref, ties = orc.filtered_ranks(name, W, X, side, positive_X, score=_oracle_score(m),
+                                           limit=getattr(m, "limit", None),
+                                           constraint=bool(getattr(m, "constraint", False)))
+            _check(got, ref, ties)
+
+
+@pytest.mark.parametrize("name", ["TransE", "DistMult", "RotatE"])
+def test_rank_fb15k237_slice_matches_oracle(name):
+    """FB15k-237 (E = 14,541), d = 200 random weights, 200 triples per side
+    filtered by the whole training set: kge_rank == the float64 oracle up to
+    near-ties."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import kge_oracle as orc
+    from KGE import ranking, score
+    z = np.load(os.path.join(ROOT, "data", "fb15k237_train.npz"))
+    T = z["triples"].astype(np.int64)
+    E, R = int(z["n_entities"]), int(z["n_relations"])
+    sc = None if name == "DistMult" else score.LpDistance(2)
+    m = build(name, sc, embedding_params={"embedding_size": 200})
+    m.metadata = {"ind2ent": list(range(E)), "ind2rel": list(range(R))}
+    m._model_weights_initial = None
+    m._init_embeddings(seed=11)
+    m._to_device()
+    X = T[np.random.default_rng(4).choice(len(T), 200, replace=False)]
+    W = _oracle_weights(m)
+    PX = torch.as_tensor(T, device=m.model_weights["ent_emb"].device)
+    for side in ("h", "t"):
+        got = ranking.batched_ranks(m, X, side, PX)
+        ref, ties = orc.filtered_ranks(name, W, X, side, T, score=_oracle_score(m),
+                                       limit=getattr(m, "limit", None),
+                                       constraint=bool(getattr(m, "constraint", False)))
+        _check(got, ref, ties)
+        assert (got > 1).any()
