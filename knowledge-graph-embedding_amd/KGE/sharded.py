@@ -589,12 +589,16 @@ class ShardedStep:
         self._own = None   # (its buffers point into the old table)
         if hasattr(self, "_sf"):
             self._sf = None
+        # the plan's per-step zero state (hash table, per-owner counts, error
+        # flag) in one buffer: one fill per step instead of three launches
+        zb = -(-(G * 4) // 8) * 8
+        zero = torch.zeros(hs * 8 + zb + 8, dtype=torch.uint8, device=dev)
         b = {"n_occ": n_occ, "dtype": idx_dtype, "cap": cap, "ext": ext, "hslots": hs, "pos_rows": pos_rows,
-             "pos_base": self.Es + G * cap,
-             "htab": torch.zeros(hs, dtype=torch.int64, device=dev),
-             "req_cnt": torch.zeros(G, dtype=torch.int32, device=dev),
+             "pos_base": self.Es + G * cap, "zero": zero,
+             "htab": zero[:hs * 8].view(torch.int64),
+             "req_cnt": zero[hs * 8:hs * 8 + G * 4].view(torch.int32),
              "req_ids": torch.zeros(G * cap, dtype=idx_dtype, device=dev),
-             "err": torch.zeros(1, dtype=torch.float32, device=dev)}
+             "err": zero[hs * 8 + zb:hs * 8 + zb + 4].view(torch.float32)}
         if G > 1:
             b["recv_cnt"] = torch.zeros(G, dtype=torch.int32, device=dev)
             b["recv_ids"] = torch.zeros(G * cap, dtype=idx_dtype, device=dev)
@@ -663,9 +667,7 @@ class ShardedStep:
         cap, ext, C = b["cap"], b["ext"], self.C
         st = _hip.stream_handle(self.device)
         # 1. plan: the triples / negatives in extended-table rows, request blocks
-        b["htab"].zero_()
-        b["req_cnt"].zero_()
-        b["err"].zero_()
+        b["zero"].zero_()   # htab | req_cnt | err
         lpos = torch.empty_like(batch)
         lneg = torch.empty_like(neg)
         x = _hip.kge_exchange_desc()
@@ -844,9 +846,7 @@ class ShardedStep:
         st = _hip.stream_handle(self.device)
         loop = self.loopback
         # 1. the positives' rows: plan (no negatives), requests, owners gather, rows back
-        b["htab"].zero_()
-        b["req_cnt"].zero_()
-        b["err"].zero_()
+        b["zero"].zero_()   # htab | req_cnt | err
         lpos = torch.empty_like(batch)
         x = _hip.kge_exchange_desc()
         x.abi_version = _hip.ABI_VERSION

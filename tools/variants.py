@@ -20,7 +20,8 @@ def build(name, defines, full=False):
         import __graft_entry__
         sources, defines = __graft_entry__.SOURCES, list(defines)
     else:
-        sources, defines = ("kge_step.hip", "kge_abi.hip", "kge_transr.hip", "kge_rel.hip", "kge_stream.hip", "kge_exchange.hip"), \
+        sources, defines = ("kge_step.hip", "kge_abi.hip", "kge_transr.hip", "kge_rel.hip", "kge_stream.hip", "kge_exchange.hip",
+                            "kge_owner_transe.hip", "kge_owner_other.hip"), \
             ["-DKGE_ONLY_ONE"] + list(defines)
     for src in sources:
         obj = "/tmp/var_%s_%s" % (name, src.replace(".hip", ".o"))
