@@ -488,17 +488,14 @@ class KGEModel:
                 d.all_reduce(hi, op=d.ReduceOp.MAX)
             width = (hi - lo) / bucket_count
             width = torch.where(width > 0, width, torch.ones_like(width))   # (one value: one bucket, below)
-            # bucket k = clamp(floor((x - lo) / width), 0, bc - 1): with y = (x - lo) / width >= 0,
-            # floor(y) >= k <=> y >= k, so ge[k] = #(y >= k) (plain reductions -- no atomics: a
-            # float64 index_add_ of millions of values into 30 bins serialises on 30 addresses)
-            ks = torch.arange(1, bucket_count, dtype=torch.float64, device=dev).unsqueeze(1)
-            ge = torch.zeros(bucket_count - 1, dtype=torch.float64, device=dev)
-            sub = max(1, min(chunk, (1 << 27) // max(bucket_count, 1)))   # bool [bc - 1, sub] <= 128 MB
-            for c0 in range(0, x.numel(), sub):
-                y = (x[c0:c0 + sub].to(torch.float64) - lo) / width
-                ge += (y.unsqueeze(0) >= ks).sum(1, dtype=torch.float64)
-            nl = torch.full((1,), float(x.numel()), dtype=torch.float64, device=dev)   # (this rank's values)
-            counts = torch.cat([nl - ge[:1], ge[:-1] - ge[1:], ge[-1:]]) if bucket_count > 1 else nl
+            # bucket k = clamp(floor((x - lo) / width), 0, bc - 1) in float64, counted by
+            # torch.bincount (integer counts: exact in any order; one pass over the chunk
+            # where the former bc - 1 threshold comparisons per value took 0.4 ms on C2)
+            counts = torch.zeros(bucket_count, dtype=torch.float64, device=dev)
+            for c0 in range(0, x.numel(), chunk):
+                y = torch.floor((x[c0:c0 + chunk].to(torch.float64) - lo) / width)
+                k = y.clamp_(0, bucket_count - 1).to(torch.int64)
+                counts += torch.bincount(k, minlength=bucket_count).to(torch.float64)
             if sharded:
                 d.all_reduce(counts)
             st = torch.cat([n, lo, hi, counts])
@@ -638,8 +635,10 @@ class KGEModel:
         X = np.asarray(eval_X) if not isinstance(eval_X, torch.Tensor) else eval_X.cpu().numpy()
         from ... import engine, ranking
         if engine.backend() != "eager" and ranking.supported(self):
-            # the whole set in one pass on the device (kge_rank)
-            ranks = list(ranking.batched_ranks(self, X, corrupt_side, positive_X))
+            # the whole set in one pass on the device (kge_rank); the int64 array
+            # goes to the metrics as is (a list of numpy scalars made each metric
+            # re-convert 17.5k objects: ~10 ms of host time per FB15k-237 side)
+            ranks = ranking.batched_ranks(self, X, corrupt_side, positive_X)
         else:
             ranks = [self.get_rank(X[k], positive_X, corrupt_side) for k in range(len(X))]
         return {
