@@ -568,11 +568,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # KGE_BENCH_BACKEND=gloo: a rehearsal of the N-rank path on fewer GPUs
+    # (ranks share devices, tensors staged through the host; timings are not
+    # the xGMI numbers) -- the driver's runs use RCCL ("nccl")
+    backend = os.environ.get("KGE_BENCH_BACKEND", "nccl")
+    ndev = max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(local % ndev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local % ndev))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", local % ndev)
     torch.cuda.set_device(dev)
 
     from KGE import _hip, engine
@@ -660,7 +668,7 @@ def main():
     ks = float(np.mean([r[1].elapsed_time(r[2]) for r in evs]))
     ku = float(np.mean([r[2].elapsed_time(r[3]) for r in evs]))
     if sharded:
-        t = torch.tensor([ms], device=dev, dtype=torch.float64)
+        t = torch.tensor([ms], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         ms = float(t.item())
     if rank != 0:

@@ -172,8 +172,8 @@ enum {
   KGE_FLAG_OWNER_MERGE = 256,
   KGE_FLAG_DEBUG_NO_REL_SEG = 512   /* test hook: the owner merge's update pass sums the
                                        relation rows in the update kernel (one wave per
-                                       relation) instead of the per-relation segment pass;
-                                       same order, same bits */
+                                       relation) instead of the per-relation segment pass
+                                       (same sums up to their order) */
 };
 
 typedef struct kge_table {

@@ -49,7 +49,7 @@ struct Plan {
   // dense-gradient / relation-matrix models (RESCAL)
   uint64_t o_upart, o_sorted, o_srel, o_gproj, o_rpart, o_regpart, o_gent, o_grel;
   uint64_t o_gneg, o_dm;   // TransR
-  uint64_t o_leaders, o_htab, o_relseg, o_lng;
+  uint64_t o_leaders, o_htab, o_relseg, o_lng, o_rsorted, o_rsrel, o_rsbeg;
   int hbits;
   uint64_t o_gnegp, o_gpos2, o_gdense[3], o_dpart;   // TransH / TransD
   uint64_t o_owncodes;                               // owner-side scoring
@@ -474,6 +474,12 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     }
   }
   if (own) P.o_owncodes = take((uint64_t)T * 4);
+  const bool rel_seg = compact && omerge && !(d->flags & KGE_FLAG_DEBUG_NO_REL_SEG);
+  if (rel_seg) {   // launch_rel_rank's output for rel_seg_kernel
+    P.o_rsorted = take((uint64_t)B * 4);
+    P.o_rsrel = take((uint64_t)B * 4);
+    P.o_rsbeg = take((uint64_t)R * 2 * 4);
+  }
   // owner merge, SGD update pass: long destination lists deferred (kLongN)
   const bool pos_only = omerge && compact && d->optimizer == KGE_OPT_SGD && !fuse_norm_plan && entc <= 256 * kLongCPT;
   const uint32_t lng_cap = (uint32_t)(T / kLongN + 1);
@@ -711,6 +717,11 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   A.gpe_stride = 3 * A.gcols;
   A.gpe_toff = 2 * A.gcols;
   if (P.own) A.own_codes = (uint32_t*)(ws + P.o_owncodes);
+  if (A.rel_seg) {
+    A.rs_sorted = (int32_t*)(ws + P.o_rsorted);
+    A.rs_srel = (int32_t*)(ws + P.o_rsrel);
+    A.rs_beg = (int32_t*)(ws + P.o_rsbeg);
+  }
   if (P.pos_only) {
     A.pos_only = true;
     A.lng = (uint4*)(ws + P.o_lng);

@@ -31,7 +31,7 @@ constexpr int kMergeStride = kMaxWpp + 24;   // floats of per-positive merge sta
 constexpr int kSortMax = 1024;     // update kernel: longest destination list sorted in LDS (per wave)
 // owner merge update: destinations with more than kLongN (and at most
 // kLongMax) keys go to long_rows_kernel (kLongWGs workgroups, kLongU rows in flight)
-constexpr int kLongN = 64, kLongMax = 4096, kLongWGs = 64, kLongU = 32, kLongCPT = 4;   // (rows <= 1024 floats)
+constexpr int kLongN = 64, kLongMax = 4096, kLongWGs = 64, kLongU = 16, kLongCPT = 4;   // (rows <= 1024 floats)
 
 // Control block at the head of the workspace. The caller zero-fills the
 // workspace once when it allocates it; every kernel that uses a word puts it
@@ -174,6 +174,11 @@ struct StepArgs {
   // Zipf-hot relation's list (~250 keys at C5) was a serial chain there that
   // nothing else overlapped; the update kernel only empties their list slots
   bool rel_seg = false;
+  // rel_seg's relation segments (launch_rel_rank over the batch first):
+  // positives in relation order (stable), first position and count per relation
+  int32_t* rs_sorted = nullptr;
+  int32_t* rs_srel = nullptr;
+  int32_t* rs_beg = nullptr;
   // merge update (KGE_FLAG_OWNER_MERGE | PHASE_UPDATE, SGD): every key is a
   // positive's own row gradient; a destination with more than kLongN of them
   // (a Zipf-hot head or tail) is handed to long_rows_kernel (lng[], up to

@@ -1581,17 +1581,21 @@ void update_kernel(StepArgs A) {
 // ------------------------------------------------------------ long lists
 // (A.pos_only, the owner merge's update pass) One destination row per
 // workgroup iteration: its codes -- list position 0 from the leader, the
-// list, then its overflow entries -- gathered into LDS and bitonic-sorted,
-// each thread summing one column of the positives' row gradients (gpe) in
-// ascending code order with kLongU rows in flight (the update kernel's
-// order: the same bits), then the update kernel's write (raw gradient for a
-// fetched row, else the clip-scaled SGD step) and the hash slot emptied.
+// list, then its overflow entries -- gathered into LDS and bitonic-sorted.
+// The 1024 threads are four row groups of 256: group g sums the positives'
+// row gradients (gpe) of the g-th quarter of the sorted codes, kLongU rows in
+// flight per thread (up to kLongCPT columns each); the four partial rows are
+// added in group order (deterministic). Then the update kernel's write (raw
+// gradient for a fetched row, else the clip-scaled SGD step) and the hash
+// slot emptied. (One wave summing a Zipf-hot row two codes at a time was a
+// 60 us chain; one 256-thread group, 41 us.)
 template <int UNUSED>
-__global__ __launch_bounds__(256) void long_rows_kernel(StepArgs A) {
+__global__ __launch_bounds__(1024) void long_rows_kernel(StepArgs A) {
   __shared__ uint32_t s_codes[kLongMax];
+  __shared__ float s_part[3][256 * kLongCPT];
   __shared__ uint32_t s_fill;
   if (ws_refused(A.ctl, A.sig, A.status, nullptr)) return;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, grp = tid >> 8, t = tid & 255;
   const uint32_t nitems = min(A.ctl->lng_count, A.lng_cap);
   float sc = A.ctl->scale[A.sc_ent_idx];
   if (A.scale_from_norm2) sc = -A.lr * (A.clip_norm / fmaxf(sqrtf(A.norm2_out[A.sc_ent_idx]), A.clip_norm));
@@ -1603,23 +1607,23 @@ __global__ __launch_bounds__(256) void long_rows_kernel(StepArgs A) {
     const uint32_t n = (uint32_t)A.htab[li];
     const uint32_t nl = min(n, (uint32_t)A.cap);
     const uint32_t* lst = A.list + li * (int64_t)A.cap;
-    for (uint32_t q = tid; q < nl; q += 256) s_codes[q] = (KGE_COMPACT_LIST0 && q == 0u) ? w.w : lst[q];
+    for (uint32_t q = tid; q < nl; q += 1024) s_codes[q] = (KGE_COMPACT_LIST0 && q == 0u) ? w.w : lst[q];
     if (tid == 0) s_fill = nl;
     __syncthreads();
     if (n > nl) {
       const uint32_t novf = A.ctl->ovf_len;
-      for (uint32_t q = tid; q < novf; q += 256) {
+      for (uint32_t q = tid; q < novf; q += 1024) {
         const uint64_t y = A.ovf[q];
         if ((int64_t)(y >> 32) == d) s_codes[atomicAdd(&s_fill, 1u)] = (uint32_t)y;
       }
     }
     uint32_t P = 1;
     while (P < n) P <<= 1;
-    for (uint32_t q = n + tid; q < P; q += 256) s_codes[q] = 0xFFFFFFFFu;
+    for (uint32_t q = n + tid; q < P; q += 1024) s_codes[q] = 0xFFFFFFFFu;
     __syncthreads();
     for (uint32_t k = 2; k <= P; k <<= 1) {
       for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-        for (uint32_t i = tid; i < P; i += 256) {
+        for (uint32_t i = tid; i < P; i += 1024) {
           const uint32_t l = i ^ j;
           if (l > i) {
             const uint32_t a = s_codes[i], b = s_codes[l];
@@ -1629,115 +1633,108 @@ __global__ __launch_bounds__(256) void long_rows_kernel(StepArgs A) {
         __syncthreads();
       }
     }
-    // every column of this thread (kLongCPT of them) in each batch of rows
+    // this group's quarter of the sorted codes
+    const uint32_t q0 = (uint32_t)((uint64_t)n * grp / 4), q1 = (uint32_t)((uint64_t)n * (grp + 1) / 4);
     float acc[kLongCPT];
 #pragma unroll
     for (int j = 0; j < kLongCPT; ++j) acc[j] = 0.f;
-    for (uint32_t p0 = 0; p0 < n; p0 += kLongU) {
+    for (uint32_t p0 = q0; p0 < q1; p0 += kLongU) {
       float x[kLongU][kLongCPT];
 #pragma unroll
       for (int u = 0; u < kLongU; ++u) {
-        const uint32_t code = s_codes[min(p0 + (uint32_t)u, n - 1u)] - nneg;   // (positive codes only)
+        const uint32_t code = s_codes[min(p0 + (uint32_t)u, q1 - 1u)] - nneg;   // (positive codes only)
         const float* g = A.gpe + (int64_t)(code >> 2) * A.gpe_stride + ((code & 3u) == 0u ? 0 : A.gpe_toff);
 #pragma unroll
         for (int j = 0; j < kLongCPT; ++j) {
-          const int c = tid + 256 * j;
+          const int c = t + 256 * j;
           x[u][j] = c < A.ent.cols ? g[c] : 0.f;
         }
       }
 #pragma unroll
       for (int u = 0; u < kLongU; ++u)
-        if (p0 + (uint32_t)u < n) {
+        if (p0 + (uint32_t)u < q1) {
 #pragma unroll
           for (int j = 0; j < kLongCPT; ++j) acc[j] += x[u][j];
         }
     }
-    float* row = A.ent.row_w(d);
+    if (grp > 0) {
 #pragma unroll
-    for (int j = 0; j < kLongCPT; ++j) {
-      const int c = tid + 256 * j;
-      if (c >= A.ent.cols) continue;
-      if (d >= A.remote_from) row[c] = acc[j];
-      else row[c] = row[c] + acc[j] * sc;
+      for (int j = 0; j < kLongCPT; ++j) s_part[grp - 1][t + 256 * j] = acc[j];
     }
-    if (tid == 0 && !A.keep_cnt) A.htab[li] = 0ull;
-    __syncthreads();   // s_codes is rewritten by the next destination
+    __syncthreads();
+    if (grp == 0) {
+      float* row = A.ent.row_w(d);
+#pragma unroll
+      for (int j = 0; j < kLongCPT; ++j) {
+        const int c = t + 256 * j;
+        if (c >= A.ent.cols) continue;
+        const float v = ((acc[j] + s_part[0][c]) + s_part[1][c]) + s_part[2][c];
+        if (d >= A.remote_from) row[c] = v;
+        else row[c] = row[c] + v * sc;
+      }
+      if (t == 0 && !A.keep_cnt) A.htab[li] = 0ull;
+    }
+    __syncthreads();   // s_codes / s_part are rewritten by the next destination
   }
 }
 
 // ------------------------------------------------------------ relation rows
-// (A.rel_seg) One workgroup per (relation r, 256-column strip). The batch's
-// relation ids are scanned kRsChunk at a time -- every id load of a chunk in
-// flight together, coalesced (id base + k 256 + tid) -- and the positives of
-// r listed in LDS in ascending order (a ballot per (k, wave), their counts
-// prefix-summed in that order). Each thread then sums its column of those
-// positives' relation-row gradients (gpos) in list order, kRsU rows in
-// flight: the order, and so the bits, of the update kernel's ascending-code
-// sum (a Zipf-hot relation's ~300 rows take a handful of round trips instead
-// of one per two rows). Then the update kernel's relation write: the raw
-// gradient (grad / split update modes) or the clip-scaled SGD step;
-// relations with no positive are left alone (grad mode with zero_untouched:
-// a zero row). Flat rows: both fragment layouts (load_row, load_row_half)
-// keep element e at float e.
-constexpr int kRsThreads = 256, kRsK = 8, kRsChunk = kRsK * kRsThreads, kRsU = 48;
+// (A.rel_seg, the owner merge's update pass) launch_rel_rank puts the batch's
+// positives in relation order (stable: ascending positive index within a
+// relation), then one workgroup per (relation r, 256-column strip), 1024
+// threads: a relation without positives returns after one load; otherwise its
+// positions are staged in LDS kRsChunk at a time and the threads, four row
+// groups of 256, each sum their column of one quarter of them (the positives'
+// relation-row gradients, gpos), kRsU rows in flight; the partials add in
+// group order (deterministic). Then the update kernel's relation write: the
+// raw gradient (grad / split update modes) or the clip-scaled SGD step;
+// relations with no positive are left alone (grad mode with zero_untouched: a
+// zero row). Flat rows: both fragment layouts (load_row, load_row_half) keep
+// element e at float e.
+constexpr int kRsThreads = 1024, kRsChunk = 4096, kRsU = 32;
 
 template <int UNUSED>
 __global__ __launch_bounds__(kRsThreads) void rel_seg_kernel(StepArgs A) {
-  constexpr int NW = kRsThreads / KGE_WAVE;
   __shared__ int32_t s_list[kRsChunk];
-  __shared__ int32_t s_wcnt[kRsK * NW];
+  __shared__ float s_part[3][256];
   if (ws_refused(A.ctl, A.sig, A.status, nullptr)) return;
   if (A.abort_flag && *A.abort_flag != 0.f) return;
-  const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+  const int tid = threadIdx.x, grp = tid >> 8, t = tid & 255;
   const int64_t r = blockIdx.x;
   const int cols = A.rel.cols;
-  const int c = (int)blockIdx.y * kRsThreads + tid;
+  const int c = (int)blockIdx.y * 256 + t;
   const bool cv = c < cols;
+  const int64_t cnt = A.rs_beg[A.rel.rows + r];   // (rel_cnt follows rel_beg)
+  if (cnt == 0) {
+    if ((A.grad_mode || A.rel_grad) && A.zero_untouched && grp == 0 && cv) A.grel[r * (int64_t)A.rel_gcols + c] = 0.f;
+    return;
+  }
+  const int64_t beg = A.rs_beg[r];
   const float* g = A.gpos + A.gcols + (cv ? c : 0);
   const int64_t gstride = 3 * (int64_t)A.gcols;
   float acc = 0.f;
-  int64_t tot = 0;
-  for (int64_t base = 0; base < A.B; base += kRsChunk) {
-    int64_t rid[kRsK];
-#pragma unroll
-    for (int k = 0; k < kRsK; ++k) {
-      const int64_t i = base + k * kRsThreads + tid;
-      rid[k] = i < A.B ? load_idx(A.pos, i * 3 + 1, A.i64) : -1;
-    }
-    uint64_t m[kRsK];
-#pragma unroll
-    for (int k = 0; k < kRsK; ++k) {
-      m[k] = __ballot(rid[k] == r);
-      if (lane == 0) s_wcnt[k * NW + wv] = __popcll(m[k]);
-    }
+  for (int64_t base = 0; base < cnt; base += kRsChunk) {
+    const int n = (int)min<int64_t>(kRsChunk, cnt - base);
+    for (int q = tid; q < n; q += kRsThreads) s_list[q] = A.rs_sorted[beg + base + q];
     __syncthreads();
-    int n = 0;
-#pragma unroll
-    for (int k = 0; k < kRsK; ++k) {
-      int off = n;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        if (w < wv) off += s_wcnt[k * NW + w];
-        n += s_wcnt[k * NW + w];
-      }
-      if (rid[k] == r) s_list[off + __popcll(m[k] & ((1ull << lane) - 1ull))] = k * kRsThreads + tid;
-    }
-    __syncthreads();
-    for (int p0 = 0; p0 < n; p0 += kRsU) {
+    const int q0 = n * grp / 4, q1 = n * (grp + 1) / 4;
+    for (int p0 = q0; p0 < q1; p0 += kRsU) {
       float x[kRsU];
 #pragma unroll
-      for (int u = 0; u < kRsU; ++u) x[u] = cv ? g[(base + s_list[min(p0 + u, n - 1)]) * gstride] : 0.f;
+      for (int u = 0; u < kRsU; ++u) x[u] = cv ? g[(int64_t)s_list[min(p0 + u, q1 - 1)] * gstride] : 0.f;
 #pragma unroll
       for (int u = 0; u < kRsU; ++u)
-        if (p0 + u < n) acc += x[u];
+        if (p0 + u < q1) acc += x[u];
     }
-    tot += n;
-    __syncthreads();   // s_list / s_wcnt are rewritten by the next chunk
+    __syncthreads();   // s_list is rewritten by the next chunk
   }
-  if (!cv) return;
+  if (grp > 0) s_part[grp - 1][t] = acc;
+  __syncthreads();
+  if (grp != 0 || !cv) return;
+  acc = ((acc + s_part[0][t]) + s_part[1][t]) + s_part[2][t];
   if (A.grad_mode || A.rel_grad) {
-    if (tot > 0 || A.zero_untouched) A.grel[r * (int64_t)A.rel_gcols + c] = acc;
-  } else if (tot > 0) {
+    A.grel[r * (int64_t)A.rel_gcols + c] = acc;
+  } else {
     float sc = A.ctl->scale[A.sc_rel_idx];
     if (A.scale_from_norm2) sc = -A.lr * (A.clip_norm / fmaxf(sqrtf(A.norm2_out[A.sc_rel_idx]), A.clip_norm));
     float* w = A.rel.row_w(r) + c;
@@ -1746,7 +1743,19 @@ __global__ __launch_bounds__(kRsThreads) void rel_seg_kernel(StepArgs A) {
 }
 
 static inline void launch_rel_seg(const StepArgs& A, hipStream_t st) {
-  const dim3 grid((unsigned)A.rel.rows, (unsigned)((A.rel.cols + kRsThreads - 1) / kRsThreads));
+  RelArgs R{};
+  R.ent = A.ent;
+  R.rel = A.rel;
+  R.pos = A.pos;
+  R.i64 = A.i64;
+  R.B = A.B;
+  R.sorted = A.rs_sorted;
+  R.srel = A.rs_srel;
+  R.rel_beg = A.rs_beg;
+  R.rel_cnt = A.rs_beg + A.rel.rows;
+  R.status = A.status;
+  launch_rel_rank(R, st);
+  const dim3 grid((unsigned)A.rel.rows, (unsigned)((A.rel.cols + 255) / 256));
   hipLaunchKernelGGL(rel_seg_kernel<0>, grid, dim3(kRsThreads), 0, st, A);
 }
 
@@ -1784,7 +1793,7 @@ static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_
       hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
     }
     if (A.rel_seg) launch_rel_seg(A, st);
-    if (A.pos_only) hipLaunchKernelGGL(long_rows_kernel<0>, dim3(kLongWGs), dim3(256), 0, st, A);
+    if (A.pos_only) hipLaunchKernelGGL(long_rows_kernel<0>, dim3(kLongWGs), dim3(1024), 0, st, A);
   }
   return KGE_OK;
 }

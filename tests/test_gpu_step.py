@@ -1175,8 +1175,8 @@ def test_owner_merge_hot_entities(hiplib, loopback):
     are entity 7, 30 % of the tails entity 11, 60 % of the relations 0. The
     merge's update pass hands the long destinations to long_rows_kernel and
     the relation rows to rel_seg_kernel; two steps == two oracle steps, and
-    == (bit for bit) the same steps with the relation rows summed by the
-    update kernel itself (KGE_FLAG_DEBUG_NO_REL_SEG)."""
+    == (up to summation order) the same steps with the relation rows summed
+    by the update kernel itself (KGE_FLAG_DEBUG_NO_REL_SEG)."""
     import torch.distributed as dist
     from KGE import _hip, loss, optimizers, score
     from KGE.ns_strategy import UniformStrategy
@@ -1215,7 +1215,7 @@ def test_owner_merge_hot_entities(hiplib, loopback):
                 np.testing.assert_allclose(m.model_weights[kk].cpu().numpy(), v, atol=TOL, err_msg=kk)
             outs.append({kk: v.cpu().numpy() for kk, v in m.model_weights.items()})
             del st
-        for kk in outs[0]:
-            assert np.array_equal(outs[0][kk], outs[1][kk]), kk
+        for kk in outs[0]:   # (rel_seg adds four row groups' partials: equal up to summation order)
+            np.testing.assert_allclose(outs[0][kk], outs[1][kk], rtol=0, atol=1e-6, err_msg=kk)
     finally:
         dist.destroy_process_group()
