@@ -450,6 +450,16 @@ kge_status kge_stream_permutation(const kge_stream_desc* d, int64_t epoch, int32
 kge_status kge_stream_batch_perm(const kge_stream_desc* d, const int32_t* perm_lo, const int32_t* perm_hi,
                                  int64_t epoch_lo, void* stream);
 
+/* Weight-histogram counts for the per-epoch logs (BaseModel.py's
+ * tf.summary.histogram calls; TensorBoard's bucketing): for every x[i], i < n,
+ * bucket k = clamp(floor((x[i] - lo) / width), 0, buckets - 1) evaluated in
+ * double (a NaN counts in bucket 0), lo = lo_width[0], width = lo_width[1]
+ * read on the device (the caller's device-side min / max: no host round trip);
+ * counts[k] += 1 (uint64, the caller zero-fills or accumulates over chunks).
+ * 1 <= buckets <= 256. Integer counts: exact whatever the order. */
+kge_status kge_histogram(const float* x, int64_t n, const double* lo_width, int32_t buckets,
+                         unsigned long long* counts, void* stream);
+
 /*
  * Multi-GPU sparse row exchange (KGE/sharded.py; the reference has no
  * counterpart, BaseModel.py:19-21 is single-device). Entity row e lives on

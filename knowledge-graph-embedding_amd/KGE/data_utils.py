@@ -147,11 +147,14 @@ class DeviceBatcher:
     reproducible (TF is not installed); the stream semantics are.
     """
 
-    def __init__(self, data, batch_size, shuffle, seed=None, device=None, reuse_buffer=False):
+    def __init__(self, data, batch_size, shuffle, seed=None, device=None, reuse_buffer=False, chunk=1):
         """``reuse_buffer``: every batch is written into the same device buffer
         (the caller consumes a batch before drawing the next -- the training
         loop; stream order makes the overwrite safe), saving an allocation
-        per batch."""
+        per batch. ``chunk`` (with ``reuse_buffer``, shuffled, on the GPU):
+        ``chunk`` consecutive batches are gathered by one launch into a ring
+        and handed out as views of it, in order (the caller consumes them in
+        stream order, as above); the rows are the same as batch by batch."""
         host = load_triples(data)
         if host.dtype not in (torch.int32, torch.int64):
             host = host.to(torch.int64)
@@ -173,6 +176,12 @@ class DeviceBatcher:
         self._perms = {}   # epoch -> its materialised permutation (device int32 [n])
         self._spare = []
         self._fast = None  # reused buffer: (e0, e1, entry, perm e0, perm e1, stream) of the last batch
+        # ring of `chunk` batches filled by one gather (a window spans at most two epochs)
+        self.chunk = int(chunk) if (self.reuse_buffer and self.shuffle and self.device.type == "cuda" and
+                                    int(chunk) > 1 and int(chunk) * self.batch_size <= self.n) else 1
+        self._ring = None
+        self._ring_views = None
+        self._slot = 0
 
     def __iter__(self):
         return self
@@ -183,6 +192,12 @@ class DeviceBatcher:
         return stream_rows(self.n, self.seed, start, count, self.shuffle)
 
     def __next__(self):
+        if self.chunk > 1:
+            if self._ring is None or self._slot == self.chunk:
+                self._fill_ring()
+            v = self._ring_views[self._slot]
+            self._slot += 1
+            return v
         start, B = self._pos, self.batch_size
         f = self._fast
         if f is not None and start // self.n == f[0] and (start + B - 1) // self.n == f[1]:
@@ -248,8 +263,51 @@ class DeviceBatcher:
         return self.data.index_select(0, idx)
 
 
-def set_tf_iterator(data, batch_size, shuffle, buffer_size=None, seed=None, device=None, reuse_buffer=False):
+    def _fill_ring(self):
+        """The next ``chunk`` batches, one kge_stream_batch_perm launch over
+        stream positions [pos, pos + chunk B) into the ring (the same rows the
+        batch-by-batch calls give: the window is one stretch of the stream)."""
+        import ctypes
+        from . import _hip
+        L = _hip.load()
+        G, B = self.chunk, self.batch_size
+        if self._ring is None:
+            self._ring = torch.empty((G * B, 3), dtype=self.data.dtype, device=self.data.device)
+            self._ring_views = [self._ring[i * B:(i + 1) * B] for i in range(G)]
+            d = _hip.kge_stream_desc()
+            d.abi_version = _hip.ABI_VERSION
+            d.idx_dtype = _hip.IDX_I64 if self.data.dtype == torch.int64 else _hip.IDX_I32
+            d.triples = self.data.data_ptr()
+            d.n_rows = self.n
+            d.batch = G * B
+            d.seed = self.seed
+            d.shuffle = 1
+            d.out = self._ring.data_ptr()
+            self._ring_desc = d
+            self._ring_dref = ctypes.byref(d)
+        start = self._pos
+        self._pos = start + G * B
+        self._slot = 0
+        d = self._ring_desc
+        d.start = start
+        stream = ctypes.c_void_p(torch.cuda.current_stream(self.data.device).cuda_stream)
+        e0, e1 = start // self.n, (start + G * B - 1) // self.n
+        perms = self._perms
+        for e in list(perms):
+            if e < e0:   # (reused on this stream: stream order keeps it safe)
+                self._spare.append(perms.pop(e))
+        for e in (e0, e1):
+            if e not in perms:
+                t = self._spare.pop() if self._spare else torch.empty(self.n, dtype=torch.int32, device=self.data.device)
+                _hip.check(L.kge_stream_permutation(self._ring_dref, e, ctypes.c_void_p(t.data_ptr()), stream),
+                           "kge_stream_permutation")
+                perms[e] = t
+        _hip.check(L.kge_stream_batch_perm(self._ring_dref, ctypes.c_void_p(perms[e0].data_ptr()),
+                                           ctypes.c_void_p(perms[e1].data_ptr()), e0, stream), "kge_stream_batch_perm")
+
+
+def set_tf_iterator(data, batch_size, shuffle, buffer_size=None, seed=None, device=None, reuse_buffer=False, chunk=1):
     """Drop-in for ``set_tf_iterator`` (``data_utils.py:176-196``)."""
     if shuffle:
         assert buffer_size is not None, "buffer_size must be given when shuffle is True"
-    return DeviceBatcher(data, batch_size, shuffle, seed=seed, device=device, reuse_buffer=reuse_buffer)
+    return DeviceBatcher(data, batch_size, shuffle, seed=seed, device=device, reuse_buffer=reuse_buffer, chunk=chunk)

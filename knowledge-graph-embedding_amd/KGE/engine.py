@@ -390,10 +390,14 @@ class FusedStep:
         planes = self._planes
         adam = is_train and isinstance(optimizer, _opt.Adam) and not self.grad_mode
 
-        def run():
+        def run(pos=None):
+            """``pos``: the batch's device address when it is another buffer of
+            the bound one's shape and dtype (the training loop's ring views)."""
             if self._ws_sig != sig:   # another plan used the workspace in between
                 self.workspace.zero_()
                 self._ws_sig = sig
+            if pos is not None:
+                d.pos = pos
             d.sampler.offset = planes()
             rc = step(dref, st)
             if rc:

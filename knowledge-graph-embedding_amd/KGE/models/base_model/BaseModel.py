@@ -213,8 +213,10 @@ class KGEModel:
         self.seed = _shared_seed(self.seed)
         n_train = calculate_data_size(train_X)
         self._batch_count_train = int(np.ceil(n_train / self.batch_size))
+        # batches gathered up to 32 at a time into a ring (one launch instead of 32)
         train_iter = set_tf_iterator(train_X, self.batch_size, shuffle=True, buffer_size=n_train,
-                                     seed=self.seed, device=self._device, reuse_buffer=True)
+                                     seed=self.seed, device=self._device, reuse_buffer=True,
+                                     chunk=max(1, min(32, n_train // self.batch_size)))
         if val_X is not None:
             n_val = calculate_data_size(val_X)
             self._batch_count_val = int(np.ceil(n_val / self.batch_size))
@@ -267,18 +269,19 @@ class KGEModel:
         scalar, or, given ``accum`` (device float32 [1]), adds it there and
         returns None (the fused single-device step adds it in-kernel).
 
-        The training loop refills one batch buffer in place, so a single-GPU
-        fused step is bound to (buffer, optimizer, accum) once
-        (``FusedStep.bind``) and later batches are one ``kge_step`` call; the
-        binding is dropped when the plugins, the optimizer or the weight
-        tensors change."""
+        The training loop refills one batch buffer (or a ring of them, views
+        of one tensor) in place, so a single-GPU fused step is bound to
+        (buffer, optimizer, accum) once (``FusedStep.bind``) and later batches
+        are one ``kge_step`` call with the batch's address; the binding is
+        dropped when the plugins, the optimizer or the weight tensors change."""
         opt = self._optimizer if is_train else None
         if accum is not None:
             b = self.__dict__.get("_bound")
             if b is not None:
-                run = b.get((id(batch_data), is_train, id(opt), id(accum)))
-                if run is not None and run[0] == self._bind_fingerprint(opt):
-                    run[1]()
+                base = batch_data._base if batch_data._base is not None else batch_data
+                run = b.get((id(base), batch_data.shape, is_train, id(opt), id(accum)))
+                if run is not None and run[0] == self._bind_fingerprint(opt) and batch_data.is_contiguous():
+                    run[1](batch_data.data_ptr())
                     return None
         world = _world_size()
         reason = self._plan_for(opt, batch_data.shape[0] // world)
@@ -304,9 +307,10 @@ class KGEModel:
                     if len(b) >= 8:
                         b.clear()
                     # the entry holds every object whose id it is keyed or checked by
-                    # (batch, optimizer, accum, weights), so no id can be reused while it lives
-                    b[(id(batch_data), is_train, id(opt), id(accum))] = (
-                        self._bind_fingerprint(opt), run, (batch_data, opt, accum, list(self.model_weights.values())))
+                    # (batch buffer, optimizer, accum, weights), so no id can be reused while it lives
+                    base = batch_data._base if batch_data._base is not None else batch_data
+                    b[(id(base), batch_data.shape, is_train, id(opt), id(accum))] = (
+                        self._bind_fingerprint(opt), run, (base, opt, accum, list(self.model_weights.values())))
                     run()
                     return None
                 f(batch_data, is_train, opt, accum=accum)
@@ -488,14 +492,24 @@ class KGEModel:
                 d.all_reduce(hi, op=d.ReduceOp.MAX)
             width = (hi - lo) / bucket_count
             width = torch.where(width > 0, width, torch.ones_like(width))   # (one value: one bucket, below)
-            # bucket k = clamp(floor((x - lo) / width), 0, bc - 1) in float64, counted by
-            # torch.bincount (integer counts: exact in any order; one pass over the chunk
-            # where the former bc - 1 threshold comparisons per value took 0.4 ms on C2)
-            counts = torch.zeros(bucket_count, dtype=torch.float64, device=dev)
-            for c0 in range(0, x.numel(), chunk):
-                y = torch.floor((x[c0:c0 + chunk].to(torch.float64) - lo) / width)
-                k = y.clamp_(0, bucket_count - 1).to(torch.int64)
-                counts += torch.bincount(k, minlength=bucket_count).to(torch.float64)
+            # bucket k = clamp(floor((x - lo) / width), 0, bc - 1) in float64; integer counts,
+            # exact in any order. On the GPU: kge_histogram, one pass, lo / width read on the
+            # device (torch.bincount sizes its output on the host: a device sync per weight,
+            # ~20 ms of host stall per epoch on C2)
+            if dev.type == "cuda" and x.dtype == torch.float32:
+                from ... import _hip
+                lw = torch.cat([lo, width])
+                c64 = torch.zeros(bucket_count, dtype=torch.int64, device=dev)
+                xc = x.contiguous()
+                _hip.check(_hip.lib().kge_histogram(_hip.ptr(xc), xc.numel(), _hip.ptr(lw), bucket_count,
+                                                    _hip.ptr(c64), _hip.stream_handle(dev)), "kge_histogram")
+                counts = c64.to(torch.float64)
+            else:
+                counts = torch.zeros(bucket_count, dtype=torch.float64, device=dev)
+                for c0 in range(0, x.numel(), chunk):
+                    y = torch.floor((x[c0:c0 + chunk].to(torch.float64) - lo) / width)
+                    k = y.nan_to_num_(0.0).clamp_(0, bucket_count - 1).to(torch.int64)
+                    counts += torch.bincount(k, minlength=bucket_count).to(torch.float64)
             if sharded:
                 d.all_reduce(counts)
             st = torch.cat([n, lo, hi, counts])

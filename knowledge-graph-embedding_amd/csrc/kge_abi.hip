@@ -667,6 +667,15 @@ kge_status kge_stream_batch_perm(const kge_stream_desc* d, const int32_t* perm_l
   return hip_check("kge_stream_batch_perm");
 }
 
+kge_status kge_histogram(const float* x, int64_t n, const double* lo_width, int32_t buckets,
+                         unsigned long long* counts, void* stream) {
+  if (n < 0 || buckets < 1 || buckets > 256) return fail(KGE_EINVAL, "kge_histogram: n >= 0, 1 <= buckets <= 256");
+  if (n == 0) return KGE_OK;
+  if (!x || !lo_width || !counts) return fail(KGE_EINVAL, "kge_histogram: null x / lo_width / counts");
+  launch_histogram(x, n, lo_width, buckets, counts, (hipStream_t)stream);
+  return hip_check("kge_histogram");
+}
+
 int32_t kge_abi_version(void) { return KGE_ABI_VERSION; }
 
 const char* kge_last_error(void) { return g_err.c_str(); }

@@ -294,6 +294,8 @@ struct RelArgs {
   bool lazy_absent;          // SGD step: absent relations' dense gradient re-derived by the apply (not stored)
 };
 void launch_rel_rank(const RelArgs& R, hipStream_t st);
+void launch_histogram(const float* x, int64_t n, const double* lw, int bc, unsigned long long* counts,
+                      hipStream_t st);   // kge_stream.hip (kge_histogram)
 void launch_rel_post(const RelArgs& R, hipStream_t st);     // dR (+ dense term, norm^2 partials)
 // train step tail: both passes' norms + the loss term, then both SGD applies in one launch
 void launch_rescal_norms(const RelArgs& P, const float* upart, int nu, float lam, float lr, float clip,

@@ -10,6 +10,8 @@
 // [0, n) (include/kge_hip.h kge_stream_desc) -- so no permutation array is
 // needed; callers that stream many batches per epoch materialise pi_e once
 // (kge_stream_permutation) and gather. Integer work only: one thread per row.
+#include <algorithm>
+
 #include "kge_step.h"
 
 namespace kge {
@@ -102,6 +104,31 @@ void launch_stream_gather(const void* tri, bool i64, int64_t n, int64_t start, i
   else
     hipLaunchKernelGGL(stream_gather_kernel<int32_t>, dim3(blocks), dim3(256), 0, st, (const int32_t*)tri, n, start,
                        batch, plo, phi, e0, (int32_t*)out);
+}
+
+// ---- weight histograms (kge_histogram): per-workgroup LDS bins, one
+// global 64-bit add per non-empty bin and workgroup
+__global__ __launch_bounds__(256) void histogram_kernel(const float* __restrict__ x, int64_t n,
+                                                        const double* __restrict__ lw, int bc,
+                                                        unsigned long long* __restrict__ counts) {
+  __shared__ unsigned int s_bin[256];
+  for (int k = threadIdx.x; k < bc; k += 256) s_bin[k] = 0u;
+  __syncthreads();
+  const double lo = lw[0], width = lw[1];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double y = floor(((double)x[i] - lo) / width);
+    const int k = !(y >= 0.0) ? 0 : (y >= (double)(bc - 1) ? bc - 1 : (int)y);
+    atomicAdd(&s_bin[k], 1u);
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < bc; k += 256)
+    if (s_bin[k]) atomicAdd(&counts[k], (unsigned long long)s_bin[k]);
+}
+
+void launch_histogram(const float* x, int64_t n, const double* lw, int bc, unsigned long long* counts,
+                      hipStream_t st) {
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 1024);
+  hipLaunchKernelGGL(histogram_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, lw, bc, counts);
 }
 
 void launch_stream(const void* tri, bool i64, int64_t n, int64_t start, int64_t batch, uint64_t seed, int shuffle,

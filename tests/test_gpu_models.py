@@ -176,3 +176,31 @@ def test_train_bound_fast_path_equals_step_sequence(opt_name, tmp_path):
     ck = torch.load(tmp_path / "ckpt.pt", weights_only=True)
     for k in m.model_weights:
         assert torch.equal(ck[k], m.model_weights[k].cpu()), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,bc", [(0, 30), (1, 30), (1000, 1), (257, 30), (3_000_001, 30), (70_000, 256)])
+def test_histogram_kernel_matches_host_bucketing(n, bc):
+    """kge_histogram (the per-epoch weight histograms, BaseModel.py's
+    tf.summary.histogram calls): counts equal numpy's clamp(floor((x - lo) /
+    width)) bucketing exactly, values below lo / above the last edge clamp, a
+    NaN counts in bucket 0, lo / width are read on the device, counts
+    accumulate into the caller's buffer."""
+    from KGE import _hip
+    g = np.random.default_rng(n + bc)
+    x = g.standard_normal(n).astype(np.float32)
+    if n > 2:
+        x[0], x[1] = np.nan, 1e30
+    lo, width = -1.25, 2.5 / bc
+    xd = torch.from_numpy(x).cuda()
+    lw = torch.tensor([lo, width], dtype=torch.float64, device="cuda")
+    c = torch.full((bc,), 5, dtype=torch.int64, device="cuda")
+    _hip.check(_hip.lib().kge_histogram(_hip.ptr(xd), n, _hip.ptr(lw), bc, _hip.ptr(c), _hip.stream_handle()),
+               "kge_histogram")
+    y = np.floor((x.astype(np.float64) - lo) / width)
+    k = np.where(np.isnan(y), 0, np.clip(np.nan_to_num(y, nan=0.0), 0, bc - 1)).astype(np.int64)
+    want = np.bincount(k, minlength=bc) + 5
+    assert np.array_equal(c.cpu().numpy(), want)
+    with pytest.raises(ValueError):
+        _hip.check(_hip.lib().kge_histogram(_hip.ptr(xd), n, _hip.ptr(lw), 257, _hip.ptr(c), _hip.stream_handle()),
+                   "kge_histogram")

@@ -180,3 +180,22 @@ def test_device_batcher_uses_perm_path_and_matches_host():
         rows = torch.from_numpy(_philox.stream_rows(n, SEED, b * 100000, 100000, 1)).cuda()
         assert torch.equal(out, host.cuda()[rows])
     assert len(it._perms) <= 2
+
+
+@pytest.mark.parametrize("n,B,G", [(272115, 1024, 32), (700, 64, 10), (1000, 100, 7)])
+def test_device_batcher_ring_equals_batch_by_batch(n, B, G):
+    """DeviceBatcher(chunk=G) (train()'s ring: G batches per gather launch)
+    hands out the same batches as chunk=1, across epoch boundaries, as views
+    of one ring tensor in order."""
+    from KGE.data_utils import DeviceBatcher
+    host = torch.arange(n * 3, dtype=torch.int64).reshape(n, 3)
+    dev = torch.device("cuda")
+    a = DeviceBatcher(host, B, shuffle=True, seed=SEED, device=dev, reuse_buffer=True, chunk=G)
+    b = DeviceBatcher(host, B, shuffle=True, seed=SEED, device=dev, reuse_buffer=True)
+    assert a.chunk == G
+    steps = max(3 * G + 1, 3 * n // B + 2)
+    for s in range(steps):
+        x, y = next(a), next(b)
+        assert x._base is a._ring and x.is_contiguous()
+        assert torch.equal(x, y), s
+    assert len(a._perms) <= 2
