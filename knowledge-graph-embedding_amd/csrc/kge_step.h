@@ -31,7 +31,13 @@ constexpr int kMergeStride = kMaxWpp + 24;   // floats of per-positive merge sta
 constexpr int kSortMax = 1024;     // update kernel: longest destination list sorted in LDS (per wave)
 // owner merge update: destinations with more than kLongN (and at most
 // kLongMax) keys go to long_rows_kernel (kLongWGs workgroups, kLongU rows in flight)
-constexpr int kLongN = 64, kLongMax = 4096, kLongWGs = 64, kLongU = 16, kLongCPT = 4;   // (rows <= 1024 floats)
+#ifndef KGE_LONG_N
+#define KGE_LONG_N 64   // (tuning knob)
+#endif
+#ifndef KGE_LONG_WGS
+#define KGE_LONG_WGS 64   // (tuning knob)
+#endif
+constexpr int kLongN = KGE_LONG_N, kLongMax = 4096, kLongWGs = KGE_LONG_WGS, kLongU = 16, kLongCPT = 4;   // (rows <= 1024 floats)
 
 // Control block at the head of the workspace. The caller zero-fills the
 // workspace once when it allocates it; every kernel that uses a word puts it

@@ -48,9 +48,9 @@ def run(names, extra=()):
             print(n, "FAILED", out.stderr[-800:])
             continue
         d = json.loads(line[-1])
-        k = d["roofline"]["kernels"]
-        print("%-12s %.5f ms/step  KS %.5f  KU %.5f" % (n, d["ms_per_step"], k["score_kernel"]["ms"],
-                                                        k["update_kernel"]["ms"]), flush=True)
+        k = (d.get("roofline") or {}).get("kernels") or {}
+        ks, ku = (k.get("score_kernel") or {}).get("ms"), (k.get("update_kernel") or {}).get("ms")
+        print("%-12s %.5f ms/step  KS %s  KU %s" % (n, d["ms_per_step"], ks, ku), flush=True)
 
 
 if __name__ == "__main__":
