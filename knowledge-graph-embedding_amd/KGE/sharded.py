@@ -598,7 +598,9 @@ class ShardedStep:
              "htab": zero[:hs * 8].view(torch.int64),
              "req_cnt": zero[hs * 8:hs * 8 + G * 4].view(torch.int32),
              "req_ids": torch.zeros(G * cap, dtype=idx_dtype, device=dev),
-             "err": zero[hs * 8 + zb:hs * 8 + zb + 4].view(torch.float32)}
+             "err": zero[hs * 8 + zb:hs * 8 + zb + 4].view(torch.float32),
+             # [exchange plan's flag | owner pass's flag], zeroed with the rest
+             "errs": zero[hs * 8 + zb:hs * 8 + zb + 8].view(torch.float32)}
         if G > 1:
             b["recv_cnt"] = torch.zeros(G, dtype=torch.int32, device=dev)
             b["recv_ids"] = torch.zeros(G * cap, dtype=idx_dtype, device=dev)
@@ -792,7 +794,7 @@ class ShardedStep:
              "gtrip": torch.zeros(G * Bn, 3, dtype=idx_dtype, device=dev),
              "gneg": torch.zeros(G * Bn * Keff, dtype=idx_dtype, device=dev) if given else None,
              "stats": torch.zeros(G * Bn, 4, dtype=torch.float32, device=dev),
-             "err": torch.zeros(1, dtype=torch.float32, device=dev)}
+             "err": b["errs"][1:]}   # (zeroed per step by b["zero"])
         fo.plane_fn = lambda ns, n: o["base_plane"]   # rank 0's planes of this step (set per step)
         common = {"world": G, "rank": g, "batch": Bn}
         fo.owner = dict(common, rows_from=b["pos_base"], global_entities=self.E, err=o["err"], stats=o["stats"])
@@ -889,7 +891,6 @@ class ShardedStep:
             ev_s = (ctypes.c_void_p * 4)(prof_events[0], prof_events[1], prof_events[2], sc[0])
             ev_u = (ctypes.c_void_p * 4)(sc[0], sc[1], sc[2], prof_events[3])
         fo, fm = o["fo"], o["fm"]
-        o["err"].zero_()
         fo.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER | _hip.FLAG_PHASE_SCORE
         opt = optimizer if is_train else None
         fo(o["gtrip"], is_train, opt, neg_ids=o["gneg"], prof_events=ev_s)
@@ -900,7 +901,7 @@ class ShardedStep:
         fm(lpos, is_train, opt)
         # 6. [norm^2 x4 | loss | - | - | error flag], the stats
         small = self.red[-8:]
-        torch.maximum(b["err"], o["err"], out=small[-1:])
+        torch.amax(b["errs"], dim=0, keepdim=True, out=small[-1:])
         if G > 1:
             ex.all_reduce(small)
             ex.all_gather(o["stats"], o["stats_mine"])

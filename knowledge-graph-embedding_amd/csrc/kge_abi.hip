@@ -744,7 +744,8 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     if (ev) { (void)hipEventRecord(ev[0], st); (void)hipEventRecord(ev[1], st); }
     const bool upd = d->flags & KGE_FLAG_PHASE_UPDATE;
     if (d->batch > 0) {
-      if (P.omerge && upd)   // its relation gradients start from zero
+      // its relation gradients start from zero (rel_seg writes every row's every column itself)
+      if (P.omerge && upd && !(A.rel_seg && A.rel_gcols == A.rel.cols))
         (void)hipMemsetAsync(d->grad_out[1], 0, (size_t)A.rel.rows * A.rel_gcols * sizeof(float), st);
       const int phase = upd ? 1 : P.own ? 0 : 2;
       if (!upd || P.own) {

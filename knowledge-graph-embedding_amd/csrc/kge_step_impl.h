@@ -1688,8 +1688,8 @@ __global__ __launch_bounds__(1024) void long_rows_kernel(StepArgs A) {
 // relation-row gradients, gpos), kRsU rows in flight; the partials add in
 // group order (deterministic). Then the update kernel's relation write: the
 // raw gradient (grad / split update modes) or the clip-scaled SGD step;
-// relations with no positive are left alone (grad mode with zero_untouched: a
-// zero row). Flat rows: both fragment layouts (load_row, load_row_half) keep
+// relations with no positive get a zero gradient row (grad / relation-gradient
+// modes) or are left alone (SGD). Flat rows: both fragment layouts (load_row, load_row_half) keep
 // element e at float e.
 constexpr int kRsThreads = 1024, kRsChunk = 4096, kRsU = 32;
 
@@ -1706,7 +1706,8 @@ __global__ __launch_bounds__(kRsThreads) void rel_seg_kernel(StepArgs A) {
   const bool cv = c < cols;
   const int64_t cnt = A.rs_beg[A.rel.rows + r];   // (rel_cnt follows rel_beg)
   if (cnt == 0) {
-    if ((A.grad_mode || A.rel_grad) && A.zero_untouched && grp == 0 && cv) A.grel[r * (int64_t)A.rel_gcols + c] = 0.f;
+    // (every relation row of grel is written here: the caller skips its zero-fill)
+    if ((A.grad_mode || A.rel_grad) && grp == 0 && cv) A.grel[r * (int64_t)A.rel_gcols + c] = 0.f;
     return;
   }
   const int64_t beg = A.rs_beg[r];
