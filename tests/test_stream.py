@@ -96,3 +96,17 @@ def test_stream_abi_rejects_without_gpu(hiplib, field, value, msg):
     setattr(d, field, value)
     assert hiplib.kge_stream_batch(ctypes.byref(d), None) == _hip.KGE_EINVAL
     assert msg in hiplib.kge_last_error().decode()
+
+
+def test_batcher_ring_only_where_it_applies():
+    """DeviceBatcher(chunk=G) gathers G batches per launch only on the GPU
+    (shuffled, reused buffer, G B <= n: tests/test_gpu_stream.py); on the CPU
+    it is the batch-by-batch stream, the same rows."""
+    from KGE.data_utils import DeviceBatcher
+    host = torch.arange(700 * 3, dtype=torch.int64).reshape(700, 3)
+    cpu = torch.device("cpu")
+    a = DeviceBatcher(host, 64, shuffle=True, seed=5, device=cpu, reuse_buffer=True, chunk=10)
+    b = DeviceBatcher(host, 64, shuffle=True, seed=5, device=cpu)
+    assert a.chunk == 1
+    for _ in range(25):
+        assert torch.equal(next(a), next(b))
