@@ -27,6 +27,14 @@
  *    table or an output, the status word gets KGE_EWORKSPACE and *loss_out is
  *    NaN. Re-zero the workspace (or allocate a zeroed one) whenever the
  *    signature changes.
+ *  - Split steps (KGE_FLAG_PHASE_SCORE, then KGE_FLAG_PHASE_UPDATE): the
+ *    update pass consumes what its score pass left in the workspace, so a
+ *    PHASE_UPDATE call runs only after a PHASE_SCORE call of the same plan on
+ *    the same workspace, once. One that finds no such pending score pass (a
+ *    fresh or re-zeroed workspace, a second update, another plan's score
+ *    pass) is REFUSED on the device: no table written, status KGE_EWORKSPACE,
+ *    and the workspace stays refused for every later step until the caller
+ *    zero-fills it (then: PHASE_SCORE again).
  *  - Calls are stream-ordered, re-entrant and never throw. They return a
  *    kge_status; kge_last_error() gives a thread-local message.
  *  - Device-side range violations (entity / relation ids out of range) are
@@ -139,7 +147,10 @@ enum {
    *                 to their owner), the others the clipped SGD update;
    *                 relation rows' summed raw gradients go to grad_out[1]
    *                 (zero-filled by the call) for the caller to reduce and apply;
-   *                 nothing at all when abort_flag is set and *abort_flag != 0. */
+   *                 nothing at all when abort_flag is set and *abort_flag != 0.
+   *                 Refused (KGE_EWORKSPACE) unless this plan's PHASE_SCORE
+   *                 call ran on the workspace since the last update pass (see
+   *                 the ABI rules above). */
   KGE_FLAG_PHASE_SCORE = 32,
   KGE_FLAG_PHASE_UPDATE = 64,
   /* Owner-side scoring (the multi-GPU "owner" step, KGE/sharded.py; TransE /
@@ -300,7 +311,7 @@ typedef struct kge_step_desc {
   float* owner_stats_out;     /* OWNER_MERGE | PHASE_SCORE: [batch, 4] out      */
   int64_t owner_key_capacity; /* OWNER: key positions for the owned negatives (0: 5/4 of the
                                  expected owner_batch * K_eff, + 4096)          */
-  float* owner_err;           /* OWNER: set to 1 when the owned negatives exceed the capacity
+  float* owner_err;           /* OWNER: set to 2 when the owned negatives exceed the capacity
                                  (their keys are dropped: the caller voids the step; nullable) */
 } kge_step_desc;
 
@@ -459,6 +470,13 @@ kge_status kge_stream_batch_perm(const kge_stream_desc* d, const int32_t* perm_l
  * 1 <= buckets <= 256. Integer counts: exact whatever the order. */
 kge_status kge_histogram(const float* x, int64_t n, const double* lo_width, int32_t buckets,
                          unsigned long long* counts, void* stream);
+
+/* Device copy of n16 16-byte elements, src -> dst (non-overlapping, both
+ * 16-byte aligned): each lane moves four float4s, every load issued before any
+ * store. A plain streaming copy: bench.py times it on a buffer far larger than
+ * the Infinity Cache as the box's measured HBM copy peak, the second
+ * denominator of the step's roofline fraction. */
+kge_status kge_copy16(const void* src, void* dst, int64_t n16, void* stream);
 
 /*
  * Multi-GPU sparse row exchange (KGE/sharded.py; the reference has no

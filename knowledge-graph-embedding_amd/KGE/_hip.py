@@ -144,7 +144,7 @@ EXPORTS = ("kge_abi_version", "kge_last_error", "kge_step_workspace_bytes", "kge
            "kge_sample",
            "kge_apply", "kge_apply_many", "kge_constrain_rows", "kge_rank", "kge_apply_rows", "kge_stream_batch",
            "kge_stream_permutation", "kge_stream_batch_perm", "kge_exchange_plan",
-           "kge_exchange_rows", "kge_owner_record_floats", "kge_histogram")
+           "kge_exchange_rows", "kge_owner_record_floats", "kge_histogram", "kge_copy16")
 
 _lock = threading.Lock()
 _lib = None
@@ -192,6 +192,8 @@ def load(path=LIB_PATH):
         L.kge_histogram.restype = ctypes.c_int
         L.kge_histogram.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                                     ctypes.c_void_p, ctypes.c_void_p]
+        L.kge_copy16.restype = ctypes.c_int
+        L.kge_copy16.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
         L.kge_exchange_plan.restype = ctypes.c_int
         L.kge_exchange_plan.argtypes = [ctypes.POINTER(kge_exchange_desc), ctypes.c_void_p]
         L.kge_exchange_rows.restype = ctypes.c_int

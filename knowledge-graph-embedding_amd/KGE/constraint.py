@@ -1,7 +1,10 @@
 """Constraint / regulariser helpers (reference ``KGE/constraint.py:4-126``).
 
 Torch restatements used by the eager plugin path and by ``_init_embeddings``;
-the fused HIP step implements the same formulas in ``csrc/kge_constraint.hip``.
+the fused HIP step implements the same formulas in ``csrc/kge_step.hip``
+(``constrain_rows_kernel``: normalise / clip rows), fused into the score / update
+kernels (``csrc/kge_step_impl.h``, ``fuse_norm``), ``csrc/kge_proj.hip`` (TransH soft /
+orthogonality terms) and ``csrc/kge_rel.hip`` (RESCAL Lp regulariser).
 """
 
 import math

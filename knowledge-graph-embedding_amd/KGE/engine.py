@@ -269,6 +269,7 @@ class FusedStep:
             d.owner_world, d.owner_rank, d.owner_batch = o["world"], o["rank"], o["batch"]
             d.owner_rows_from = o.get("rows_from", 0)
             d.global_entities = o.get("global_entities", 0)
+            d.owner_key_capacity = int(o.get("key_capacity", 0))
             for f in ("records", "stats", "stats_out", "err"):
                 if o.get(f) is not None:
                     setattr(d, "owner_" + f, o[f].data_ptr())

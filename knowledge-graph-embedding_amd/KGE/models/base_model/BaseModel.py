@@ -123,6 +123,10 @@ class KGEModel:
         later. Early stopping reads the validation loss at once (its decision
         gates the next epoch)."""
         pending = None
+        # a deferred epoch's results are read once this many of the next
+        # epoch's batches are queued: the reads then wait for nothing (the GPU
+        # has ~1.5 ms of batches ahead of the host at C2's 0.08 ms per batch)
+        read_after = 15
         for i in range(epochs):
             # per-epoch loss sums stay on the device: the fused step adds each
             # batch's loss into them itself (no per-batch host work); the host
@@ -133,7 +137,7 @@ class KGEModel:
                 self._run_single_batch(next(train_iter), is_train=True, accum=train_loss)
                 if val_iter is not None and b < self._batch_count_val:
                     self._run_single_batch(next(val_iter), is_train=False, accum=val_loss)
-                if pending is not None and b >= 15:   # the GPU has this epoch's first batches queued
+                if pending is not None and b >= read_after:
                     self._finish_epoch(pending, train_loss_history, val_loss_history)
                     pending = None
             if pending is not None:
@@ -141,7 +145,10 @@ class KGEModel:
                 pending = None
             ep = self._end_epoch(i, train_loss, val_loss, val_iter is not None)
             if early_stopping_rounds is None and ep["deferred"]:
-                self._save_checkpoint()   # (pinned copies on the stream; written by a thread)
+                # (pinned copies on the stream, written by a thread -- only if
+                # the epoch's status word is clean: a failing epoch never
+                # replaces the last good checkpoint; _finish_epoch raises it)
+                self._save_checkpoint(status=ep["dev_vals"][2:3])
                 pending = ep
                 continue
             self._finish_epoch(ep, train_loss_history, val_loss_history)
@@ -179,6 +186,7 @@ class KGEModel:
             host = bufs["vals"] = torch.empty(3, dtype=torch.float32, pin_memory=True)
         host.copy_(dev_vals, non_blocking=True)
         ep["vals"] = host
+        ep["dev_vals"] = dev_vals
         ep["hist"] = self._histogram_stats(pinned=bufs)
         ev = torch.cuda.Event()
         ev.record()
@@ -289,7 +297,8 @@ class KGEModel:
             if self._fused is None:
                 if world > 1:
                     from ...sharded import ShardedStep
-                    self._fused = ShardedStep(self, batch_hint=batch_data.shape[0] // world)
+                    self._fused = ShardedStep(self, batch_hint=batch_data.shape[0] // world,
+                                              optimizer=self._optimizer)
                 else:
                     self._fused = engine.FusedStep(self)
             if world > 1:
@@ -543,14 +552,17 @@ class KGEModel:
             with open(os.path.join(path, "%s.jsonl" % name), "a") as f:
                 f.write(json.dumps({"step": step, "buckets": buckets}) + "\n")
 
-    def _save_checkpoint(self):
+    def _save_checkpoint(self, status=None):
         """``CheckpointManager(max_to_keep=1).save()`` (``BaseModel.py:248-253``).
 
         Single device: the weights are copied into pinned host buffers on the
         step stream (ordered before the next batch's updates) and a writer
         thread waits for that copy and writes the file, so the next epoch's
         batches are issued without waiting for the disk. Every reader of the
-        file (restore, the end of ``train``) joins the writer first."""
+        file (restore, the end of ``train``) joins the writer first.
+        ``status`` (device float [1], optional): the epoch's step status word,
+        copied beside the weights; the writer keeps the previous checkpoint
+        when it is nonzero (the epoch failed)."""
         os.makedirs(self.log_path, exist_ok=True)
         path = os.path.join(self.log_path, "ckpt.pt")
         self.sync_weights()   # multi-GPU: the shards are the authoritative entity rows (collective)
@@ -572,11 +584,19 @@ class KGEModel:
                 b = bufs[k] = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
             b.copy_(v.detach(), non_blocking=True)
             snap[k] = b
+        st_host = None
+        if status is not None:
+            st_host = bufs.get("_status")
+            if st_host is None:
+                st_host = bufs["_status"] = torch.empty(1, dtype=torch.float32, pin_memory=True)
+            st_host.copy_(status, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
 
         def write():
             ev.synchronize()
+            if st_host is not None and float(st_host[0]) != 0.0:
+                return   # a failed epoch: the last good checkpoint stays
             # a whole file or none: written beside, then renamed onto ckpt.pt
             # (a reader never sees a half-written checkpoint)
             torch.save(snap, path + ".tmp")

@@ -107,7 +107,7 @@ class ShardedStep:
     """Drop-in for ``FusedStep`` across G ranks (see module docstring)."""
 
     def __init__(self, model, exchange=None, mode="auto", local_fast=True, loopback=False, capacity_slack=1.1,
-                 capacity_floor=1024, batch_hint=None):
+                 capacity_floor=1024, batch_hint=None, optimizer=None):
         """``loopback`` (sparse mode): own ids too go through the exchange blocks
         (a one-GPU rehearsal of the remote path). Each owner block holds
         ceil(capacity_slack * occurrences / G) + capacity_floor rows; a step
@@ -117,7 +117,14 @@ class ShardedStep:
         (``optimizer.iterations``, hence lr_t), as the host counts steps
         before the device knows of the overflow. ``batch_hint`` (positives per rank per step) sizes the
         exchange blocks up front, so the owned rows are allocated once, at the
-        head of the extended table (no second copy of a shard that fills HBM)."""
+        head of the extended table (no second copy of a shard that fills HBM).
+        ``optimizer`` (the training optimizer, if known): "auto" takes owner-side
+        scoring only for SGD, whose steps it covers (keras Adam trains through
+        the row exchange); with it unknown, an owner-mode step sizes its
+        buffers for both passes up front, so an Adam step falling through to
+        the row exchange never re-plans a second copy of the shard. The owner
+        pass's key capacity follows ``capacity_slack`` / ``capacity_floor``
+        too (at least 5/4 of the expected owned negatives + 4096)."""
         self.model = model
         self.ex = exchange or Exchange()
         G, g = self.ex.world, self.ex.rank
@@ -149,7 +156,8 @@ class ShardedStep:
             if E * C * 4 <= DENSE_TABLE_BYTES or self.full_reg:
                 mode = "dense"
             else:
-                mode = "owner" if self.mid in _SPLIT else "sparse"
+                owner_ok = optimizer is None or isinstance(optimizer, _opt.SGD)
+                mode = "owner" if self.mid in _SPLIT and owner_ok else "sparse"
         if mode not in ("dense", "sparse", "owner"):
             raise ValueError("mode must be 'auto', 'dense', 'sparse' or 'owner'")
         if mode in ("sparse", "owner") and self.full_reg:
@@ -170,7 +178,10 @@ class ShardedStep:
             # the extended table, the fetched blocks follow -- _ext_for)
             if batch_hint and dev.type == "cuda":
                 if mode == "owner":   # blocks for the positives' rows + every rank's positive rows
-                    self._ext_for(2 * int(batch_hint), torch.int64, fill=False, pos_rows=2 * G * int(batch_hint))
+                    n = 2 * int(batch_hint)
+                    if not isinstance(optimizer, _opt.SGD):   # (a keras Adam step runs the row exchange)
+                        n = max(n, self._occurrences(int(batch_hint)))
+                    self._ext_for(n, torch.int64, fill=False, pos_rows=2 * G * int(batch_hint))
                 else:
                     self._ext_for(self._occurrences(int(batch_hint)), torch.int64, fill=False)
             else:
@@ -797,7 +808,11 @@ class ShardedStep:
              "err": b["errs"][1:]}   # (zeroed per step by b["zero"])
         fo.plane_fn = lambda ns, n: o["base_plane"]   # rank 0's planes of this step (set per step)
         common = {"world": G, "rank": g, "batch": Bn}
-        fo.owner = dict(common, rows_from=b["pos_base"], global_entities=self.E, err=o["err"], stats=o["stats"])
+        # key positions for the owned negatives: ~Bn Keff expected (1/G of the
+        # G Bn virtual positives' slots), more when ownership is skewed
+        o["key_cap"] = min(G * Bn * Keff, int(math.ceil(max(1.25, self.slack) * Bn * Keff)) + max(4096, self.cap_floor))
+        fo.owner = dict(common, rows_from=b["pos_base"], global_entities=self.E, err=o["err"], stats=o["stats"],
+                        key_capacity=o["key_cap"])
         fo.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER | _hip.FLAG_PHASE_SCORE
         # the record width of this plan, then the record buffers
         probe = fo.describe(o["gtrip"], True, _opt.SGD(0.01), neg_ids=o["gneg"])
@@ -1202,8 +1217,15 @@ class ShardedStep:
             self.direct.check_status()
         if self.fused is not None:
             _hip.check_device_status(self.status, "kge_step")
-        if self._ext is not None and float(self.xerr) != 0.0:
+        if self._ext is not None:
+            x = float(self.xerr)
+            if x == 0.0:
+                return
             self.xerr.zero_()
+            if x >= 2.0:   # (the owner pass's flag, kge_hip.h owner_err)
+                raise RuntimeError("owner-side scoring: this rank's owned negatives overflowed the owner pass's "
+                                   "%d key positions; the step was skipped on every rank -- raise capacity_slack "
+                                   "or capacity_floor" % (self._own or {}).get("key_cap", 0))
             raise RuntimeError("sparse exchange: the step's ids overflowed an owner block (capacity %d rows); "
                                "the step was skipped on every rank -- raise capacity_slack" % self._ext["cap"])
 

@@ -398,6 +398,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     }
     A.run_score = !pu;
     A.run_update = !ps;
+    A.mark_pending = ps;
     if (pu) {
       A.scale_from_norm2 = true;
       A.rel_grad = true;
@@ -502,7 +503,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     uint32_t h = 2166136261u;
     for (const int64_t v : f)
       for (int b = 0; b < 8; ++b) h = (h ^ (uint32_t)((uint64_t)v >> (8 * b) & 0xFF)) * 16777619u;
-    P.sig = h ? h : 1u;
+    P.sig = (h == 0u || h == kPoisonedSig) ? 1u : h;   // (0: a fresh workspace; kPoisonedSig: refused)
     A.sig = P.sig;
   }
   return KGE_OK;
@@ -526,6 +527,39 @@ __global__ __launch_bounds__(256) void sample_kernel(SamplerView s, const void* 
     store_idx(out, q, e, s.i64);
   }
   if (err) set_status(status, err);
+}
+
+// ------------------------------------------------------------ phase gate
+// The first launch of a PHASE_UPDATE call (include/kge_hip.h, "split step").
+// The update pass consumes the lists, coefficients and context rows its
+// PHASE_SCORE call left in the workspace; it may run only if that score pass
+// ran on this plan since the last update pass. The score pass's last
+// workgroup leaves its plan signature in ctl->score_pending; the gate takes
+// it (resets the word) and, finding none -- a fresh or re-zeroed workspace,
+// another plan's score pass, a second update pass -- stamps kPoisonedSig as
+// the workspace's plan, so every guarded kernel of the update pass (and of
+// any later step, until the caller zeroes the workspace) refuses it: status
+// KGE_EWORKSPACE, no table written. The gate also zero-fills the relation
+// gradient rows the update pass accumulates into (n floats at zero).
+__global__ __launch_bounds__(256) void phase_gate_kernel(StepCtl* ctl, uint32_t sig, int32_t* status,
+                                                         float* zero, int64_t n) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
+    zero[q] = 0.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint32_t s = ctl->plan_sig, p = ctl->score_pending;
+    ctl->score_pending = 0u;
+    if (s != sig || p != sig) {
+      // (s is another plan's: its kernels refuse the workspace anyway; 0: the
+      // update pass would claim a fresh workspace and run on empty lists)
+      if (s == 0u || s == sig) ctl->plan_sig = kPoisonedSig;
+      set_status(status, KGE_EWORKSPACE);
+    }
+  }
+}
+
+static void launch_phase_gate(StepCtl* ctl, uint32_t sig, int32_t* status, float* zero, int64_t n, hipStream_t st) {
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 256 * 4), 256));
+  hipLaunchKernelGGL(phase_gate_kernel, dim3((unsigned)blocks), dim3(256), 0, st, ctl, sig, status, zero, n);
 }
 
 // ------------------------------------------------------------ apply rows
@@ -676,6 +710,15 @@ kge_status kge_histogram(const float* x, int64_t n, const double* lo_width, int3
   return hip_check("kge_histogram");
 }
 
+kge_status kge_copy16(const void* src, void* dst, int64_t n16, void* stream) {
+  if (n16 < 0) return fail(KGE_EINVAL, "kge_copy16: n16 must be >= 0");
+  if (n16 == 0) return KGE_OK;
+  if (!src || !dst || ((uintptr_t)src | (uintptr_t)dst) & 15)
+    return fail(KGE_EINVAL, "kge_copy16: null or unaligned src / dst");
+  launch_copy16(src, dst, n16, (hipStream_t)stream);
+  return hip_check("kge_copy16");
+}
+
 int32_t kge_abi_version(void) { return KGE_ABI_VERSION; }
 
 const char* kge_last_error(void) { return g_err.c_str(); }
@@ -744,9 +787,13 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     if (ev) { (void)hipEventRecord(ev[0], st); (void)hipEventRecord(ev[1], st); }
     const bool upd = d->flags & KGE_FLAG_PHASE_UPDATE;
     if (d->batch > 0) {
-      // its relation gradients start from zero (rel_seg writes every row's every column itself)
-      if (P.omerge && upd && !(A.rel_seg && A.rel_gcols == A.rel.cols))
-        (void)hipMemsetAsync(d->grad_out[1], 0, (size_t)A.rel.rows * A.rel_gcols * sizeof(float), st);
+      // the phase gate; the merge's relation gradients start from zero
+      // (rel_seg writes every row's every column itself)
+      if (upd) {
+        const bool zero = P.omerge && !(A.rel_seg && A.rel_gcols == A.rel.cols);
+        launch_phase_gate(A.ctl, A.sig, A.status, zero ? d->grad_out[1] : nullptr,
+                          zero ? A.rel.rows * (int64_t)A.rel_gcols : 0, st);
+      }
       const int phase = upd ? 1 : P.own ? 0 : 2;
       if (!upd || P.own) {
         s = d->model == KGE_MODEL_TRANSE ? launch_owner_transe(A, P.G, P.sk, phase, st)
@@ -847,10 +894,9 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   if (ev) (void)hipEventRecord(ev[0], st);
   const bool phase_update = d->flags & KGE_FLAG_PHASE_UPDATE;
   if (phase_update) {
-    // the update pass alone (the score pass ran in the previous call): its
-    // relation gradients start from zero
-    if (d->batch > 0)
-      (void)hipMemsetAsync(d->grad_out[1], 0, (size_t)A.rel.rows * A.rel_gcols * sizeof(float), st);
+    // the update pass alone (the score pass ran in the previous call): the
+    // phase gate, which also zero-fills the relation gradients it accumulates
+    if (d->batch > 0) launch_phase_gate(A.ctl, A.sig, A.status, d->grad_out[1], A.rel.rows * (int64_t)A.rel_gcols, st);
     if (ev) (void)hipEventRecord(ev[1], st);
     if (d->batch > 0) s = launch_step_elementwise(A, P.G, d->model, P.sk, st, ev);
     if (s != KGE_OK) return fail(s, "no kernel instance for model %d / score %d", d->model, P.sk);

@@ -234,6 +234,7 @@ __global__ __launch_bounds__(kMergeWaves * KGE_WAVE) void owner_merge_kernel(Ste
       A.ctl->score_ticket = 0u;
       A.ctl->ovf_len = __hip_atomic_exchange(&A.ctl->ovf_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       A.ctl->lng_count = 0u;   // the update pass's deferred long destinations
+      A.ctl->score_pending = A.sig;   // (the merge is always a PHASE_SCORE call: the phase gate's token)
     }
   }
 }

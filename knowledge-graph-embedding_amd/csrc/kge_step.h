@@ -54,7 +54,8 @@ struct StepCtl {
   float dn2[4];            // norm^2 of the dense (duplicate-summed) gradient per variable
   float reg_r2;            // RESCAL train step: sum_r ||R_r||_F^2 (rel_dr partials)
   uint32_t plan_sig;       // signature of the plan that last used the workspace (0: fresh)
-  uint32_t pad1;
+  uint32_t score_pending;  // split step: the plan signature, set by a PHASE_SCORE pass's last
+                           // workgroup and consumed by the next PHASE_UPDATE call (phase gate)
   uint32_t own_count;      // owner score pass: key positions taken (per-workgroup blocks)
   uint32_t own_len;        // ... handed to the coefficient / update passes by the last workgroup
   uint32_t lng_count;      // merge update: long destinations deferred to long_rows_kernel (reset by the merge)
@@ -85,6 +86,10 @@ __device__ __noinline__ bool ws_refused_slow(StepCtl* ctl, uint32_t s, uint32_t 
   }
   return true;
 }
+// A plan signature no plan has (make_plan maps it away): the phase gate
+// stamps it when a PHASE_UPDATE call finds no pending score pass of its plan,
+// so every guarded kernel refuses the workspace until the caller zeroes it.
+constexpr uint32_t kPoisonedSig = 0xFFFFFFFFu;
 __device__ __forceinline__ bool ws_refused(StepCtl* ctl, uint32_t sig, int32_t* status, float* loss_out) {
   const uint32_t s = *reinterpret_cast<const uint32_t*>(&ctl->plan_sig);
   // the common case (the workspace is this plan's) is one scalar compare; the
@@ -231,6 +236,7 @@ struct StepArgs {
   uint32_t sig;     // plan signature (ws_refused)
   // split step (KGE_FLAG_PHASE_*, the multi-GPU sparse exchange)
   bool run_score = true, run_update = true;
+  bool mark_pending = false;   // PHASE_SCORE: the last score workgroup sets ctl->score_pending = sig
   bool scale_from_norm2 = false;   // update pass: clip scales from norm2_out (all-reduced by the caller)
   bool rel_grad = false;           // update pass: relation rows' raw gradients -> grel (no update)
   int64_t remote_from = INT64_MAX; // entity rows >= this: raw gradient written in place of the row
@@ -252,7 +258,7 @@ struct StepArgs {
   float* own_stats_out = nullptr;   // merge: [B, 4] out
   uint32_t* own_codes = nullptr;    // owner: [own_cap] destination code per key position (~0: padding)
   uint32_t own_cap = 0;             // owner: key positions available (grid of the update launch)
-  float* own_err = nullptr;         // owner: set to 1 when the owned keys exceed own_cap
+  float* own_err = nullptr;         // owner: set to 2 when the owned keys exceed own_cap
   bool own_keys = false;            // update kernel: compact key positions [0, ctl->own_len)
 };
 // accumulator images per owner record: M::REC_IMG when the model declares it
@@ -302,6 +308,7 @@ struct RelArgs {
 void launch_rel_rank(const RelArgs& R, hipStream_t st);
 void launch_histogram(const float* x, int64_t n, const double* lw, int bc, unsigned long long* counts,
                       hipStream_t st);   // kge_stream.hip (kge_histogram)
+void launch_copy16(const void* src, void* dst, int64_t n16, hipStream_t st);   // kge_stream.hip (kge_copy16)
 void launch_rel_post(const RelArgs& R, hipStream_t st);     // dR (+ dense term, norm^2 partials)
 // train step tail: both passes' norms + the loss term, then both SGD applies in one launch
 void launch_rescal_norms(const RelArgs& P, const float* upart, int nu, float lam, float lr, float clip,

@@ -919,7 +919,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
               A.own_codes[kpos] = code;
               bin_key(A, ids[c], code, kpos);
             } else if (A.own_err) {
-              *A.own_err = 1.f;
+              *A.own_err = 2.f;   // (2: told apart from the exchange plan's block overflow, 1)
             }
           }
         }
@@ -971,6 +971,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
         A.ctl->score_ticket = 0u;
         A.ctl->ovf_len = __hip_atomic_exchange(&A.ctl->ovf_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         A.ctl->own_len = __hip_atomic_exchange(&A.ctl->own_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        A.ctl->score_pending = A.sig;   // (the owner pass is always a PHASE_SCORE call)
       }
     }
     return;
@@ -1038,6 +1039,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
         // every workgroup's keys are filed: hand the overflow length to the
         // update kernel and restart the overflow list for the next step
         A.ctl->ovf_len = __hip_atomic_exchange(&A.ctl->ovf_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (A.mark_pending) A.ctl->score_pending = A.sig;   // the phase gate's token (kge_abi.hip)
       } else {
         A.ctl->scale[tid - 1] = -A.lr * (A.clip_norm / fmaxf(sqrtf(s), A.clip_norm));
         if (A.norm2_out) A.norm2_out[tid - 1] = s;
@@ -1698,12 +1700,18 @@ __global__ __launch_bounds__(kRsThreads) void rel_seg_kernel(StepArgs A) {
   __shared__ int32_t s_list[kRsChunk];
   __shared__ float s_part[3][256];
   if (ws_refused(A.ctl, A.sig, A.status, nullptr)) return;
-  if (A.abort_flag && *A.abort_flag != 0.f) return;
   const int tid = threadIdx.x, grp = tid >> 8, t = tid & 255;
   const int64_t r = blockIdx.x;
   const int cols = A.rel.cols;
   const int c = (int)blockIdx.y * 256 + t;
   const bool cv = c < cols;
+  if (A.abort_flag && *A.abort_flag != 0.f) {
+    // an aborted step: no table written, but every relation gradient row is
+    // still this kernel's to write (the caller skipped the zero-fill) -- zeros,
+    // never the previous step's values
+    if ((A.grad_mode || A.rel_grad) && grp == 0 && cv) A.grel[r * (int64_t)A.rel_gcols + c] = 0.f;
+    return;
+  }
   const int64_t cnt = A.rs_beg[A.rel.rows + r];   // (rel_cnt follows rel_beg)
   if (cnt == 0) {
     // (every relation row of grel is written here: the caller skips its zero-fill)

@@ -131,6 +131,27 @@ void launch_histogram(const float* x, int64_t n, const double* lw, int bc, unsig
   hipLaunchKernelGGL(histogram_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, lw, bc, counts);
 }
 
+// ---- kge_copy16: the streaming copy bench.py measures the HBM peak with
+__global__ __launch_bounds__(256) void copy16_kernel(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                     int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += 4 * stride) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * stride < n) v[u] = src[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i + u * stride < n) dst[i + u * stride] = v[u];
+  }
+}
+
+void launch_copy16(const void* src, void* dst, int64_t n16, hipStream_t st) {
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>((n16 + 1023) / 1024, 1), 256 * 32);
+  hipLaunchKernelGGL(copy16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float4*)src, (float4*)dst,
+                     n16);
+}
+
 void launch_stream(const void* tri, bool i64, int64_t n, int64_t start, int64_t batch, uint64_t seed, int shuffle,
                    void* out, hipStream_t st) {
   const int w = 2 * stream_half_bits(n);

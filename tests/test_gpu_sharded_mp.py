@@ -97,3 +97,83 @@ def test_two_ranks_one_gpu_equal_oracle(hiplib, name, loss, opt, mode, loopback)
     assert abs(got_loss - ref["loss"]) <= 1e-5 * max(1.0, abs(ref["loss"]))
     for k, v in ref_w.items():
         np.testing.assert_allclose(got[k], v, atol=1e-5, err_msg=k)
+
+
+# owner-side scoring at a bench-like shape: two ranks on one GPU, in-kernel draws
+OE, OR, OD, OB, OK = 60_000, 40, 200, 128, 64
+
+
+def _owner_case():
+    rng = np.random.default_rng(77)
+    lim = 6.0 / np.sqrt(OD)
+    W = {"ent_emb": rng.uniform(-lim, lim, (OE, OD)).astype(np.float32),
+         "rel_emb": rng.uniform(-lim, lim, (OR, OD)).astype(np.float32)}
+    pos = [np.stack([rng.integers(0, OE, 2 * OB), rng.integers(0, OR, 2 * OB), rng.integers(0, OE, 2 * OB)], 1)
+           for _ in range(2)]
+    return W, pos
+
+
+def _owner_worker(rank, port, out):
+    import torch.distributed as dist
+    import __graft_entry__  # noqa: F401
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=2)
+    from KGE import loss, optimizers, score
+    from KGE.models.translating_based.TransE import TransE
+    from KGE.ns_strategy import UniformStrategy
+    from KGE.sharded import ShardedStep
+    dev = torch.device("cuda", 0)
+    W, pos = _owner_case()
+    m = TransE({"embedding_size": OD}, OK, "h+t", score_fn=score.LpDistance(2),
+               loss_fn=loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
+               ns_strategy=UniformStrategy(np.arange(OE), seed=3), constraint=True)
+    m.metadata = {"ind2ent": list(range(OE)), "ind2rel": list(range(OR))}
+    m.model_weights = {k: torch.tensor(v, device=dev) for k, v in W.items()}
+    st = ShardedStep(m, mode="owner", batch_hint=OB)
+    assert st.mode == "owner" and st.fused is not None
+    o = optimizers.SGD(0.05)
+    losses = []
+    for p in pos:
+        losses.append(float(st(torch.tensor(p[rank * OB:(rank + 1) * OB], device=dev), True, o)))
+    torch.cuda.synchronize()
+    st.check_status()
+    st.sync()
+    if rank == 0:
+        out.put(({k: v.detach().cpu().numpy().copy() for k, v in m.model_weights.items()}, losses))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_one_gpu_owner_bench_shape(hiplib):
+    """Owner-side scoring across two ranks at d = 200, K = 64 'h+t' (C2 / C4's
+    row width and a multi-wave negative count), 2 x 128 positives, 60k
+    entities (ranks own 30k rows each), renormalisation constraint, SGD, the
+    negatives drawn IN the owner pass from each positive's own rank's counter
+    planes (offset + q * 2, KGE/sharded.py) -- two steps == two single-device
+    oracle steps on the concatenated batch with those draws."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_owner_worker, args=(r, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    try:
+        got, got_losses = q.get(timeout=150)
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.exitcode is None:
+                p.kill()
+    for p in ps:
+        assert p.exitcode == 0
+    W, pos = _owner_case()
+    ref_w = W
+    for s, P in enumerate(pos):
+        base = s * 2 * 2        # take_planes(2) * G
+        neg = np.concatenate([orc.negatives(P[q * OB:(q + 1) * OB], OK, "h+t", OE, seed=3, plane=base + 2 * q)
+                              for q in range(2)])
+        ref = orc.train_step("TransE", ref_w, P, neg, score=("lp", 2.0), loss=("sans", 3.0, 1.0), lr=0.05,
+                             constraint=True, side="h+t")
+        ref_w = ref["weights"]
+        assert abs(got_losses[s] - ref["loss"]) <= 1e-5 * max(1.0, abs(ref["loss"])), s
+    for k, v in ref_w.items():
+        np.testing.assert_allclose(got[k], v, atol=1e-5, err_msg=k)

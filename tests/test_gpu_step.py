@@ -769,6 +769,71 @@ def test_replan_on_dirty_workspace_is_refused(hiplib, model_name):
         np.testing.assert_allclose(m.model_weights[kk].cpu().numpy(), v, atol=TOL, err_msg=kk)
 
 
+def test_update_phase_needs_its_score_pass(hiplib):
+    """include/kge_hip.h split-step rule, enforced by the library through the
+    C-ABI (no engine guard in the way): a KGE_FLAG_PHASE_UPDATE call runs only
+    after a PHASE_SCORE call of its plan on the same workspace, once. Refused
+    on the device (status KGE_EWORKSPACE, no table written) -- on a fresh
+    workspace; after the score pass's workspace was re-zeroed (the silent
+    no-op of the round-4 review); and for a second update. A refusal leaves
+    the workspace refused (even a score pass) until it is zeroed; then score
+    + update equal the oracle's SGD step (entity rows; relation gradients go
+    to grad_out[1])."""
+    import ctypes
+    from KGE import _hip, engine, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    dev = _dev()
+    rng = np.random.default_rng(61)
+    E, R, d, B, K = 40, 5, 24, 8, 4
+    W = _weights("TransE", E, R, d, rng)
+    m = _make("TransE", d, K, "h+t", score.LpDistance(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E, R,
+              UniformStrategy(np.arange(E), seed=3), constraint=False)
+    m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
+    step = engine.FusedStep(m)
+    step.rel_grad_out = torch.zeros(R, d, device=dev)
+    lib, st = _hip.lib(), _hip.stream_handle(dev)
+    opt = optimizers.SGD(0.05)
+    pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+    bt = torch.tensor(pos, device=dev)
+    ws = None
+
+    def run(phase):
+        nonlocal ws
+        step.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | phase
+        dd = step.describe(bt, True, opt)
+        dd.sampler.offset = 0
+        if ws is None:
+            ws = torch.zeros(int(lib.kge_step_workspace_bytes(dd)), dtype=torch.uint8, device=dev)
+        dd.workspace, dd.workspace_bytes = ws.data_ptr(), ws.numel()
+        step.status.zero_()
+        assert lib.kge_step(ctypes.byref(dd), st) == _hip.KGE_OK
+        torch.cuda.synchronize()
+        return int(step.status.item())
+
+    def unchanged():
+        for kk, v in W.items():
+            assert np.array_equal(m.model_weights[kk].cpu().numpy(), v), kk
+
+    S, U = _hip.FLAG_PHASE_SCORE, _hip.FLAG_PHASE_UPDATE
+    assert run(U) == _hip.KGE_EWORKSPACE            # fresh workspace, no score pass
+    unchanged()
+    ws.zero_()
+    assert run(S) == _hip.KGE_OK
+    ws.zero_()                                       # the score pass's lists wiped
+    assert run(U) == _hip.KGE_EWORKSPACE
+    unchanged()
+    assert run(S) == _hip.KGE_EWORKSPACE             # refused until zeroed
+    ws.zero_()
+    assert run(S) == _hip.KGE_OK and run(U) == _hip.KGE_OK
+    neg = orc.negatives(pos, K, "h+t", E, seed=3, plane=0)
+    ref = orc.train_step("TransE", W, pos, neg, score=("lp", 2.0), loss=("sans", 3.0, 1.0), lr=0.05,
+                         constraint=False)
+    np.testing.assert_allclose(m.model_weights["ent_emb"].cpu().numpy(), ref["weights"]["ent_emb"], atol=TOL)
+    after = m.model_weights["ent_emb"].clone()
+    assert run(U) == _hip.KGE_EWORKSPACE             # a second update pass
+    assert torch.equal(m.model_weights["ent_emb"], after)
+
+
 def test_hinge_zero_negatives_is_nan(hiplib):
     from KGE import loss, score
     ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransE", 16, 5, 1, "h+t", score.LpDistance(2),
@@ -841,6 +906,51 @@ def test_fb15k237_bench_shape_properties(hiplib):
     assert math.isfinite(outs[0][0])
     assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
     assert bool(torch.isfinite(outs[0][1]).all()) and float(outs[0][3][0]) > 0
+
+
+@pytest.mark.parametrize("idx", [torch.int64, torch.int32])
+def test_transe_c2_full_size(hiplib, idx):
+    """C2 exactly as the bench times it (BASELINE configs[1];
+    BaseModel.py:293-330, TransE.py:127-174, loss.py:174-182): TransE d = 200,
+    B = 1024 real FB15k-237 positives, K = 256 'h+t' in-kernel uniform draws,
+    SANS(3, 1), LpDistance(2), constraint (the full-table unit-L2
+    renormalisation, fused into the score / update kernels on the SGD path),
+    SGD lr 0.01, E = 14,505, R = 237, the reference initialiser's range
+    U(+-6/sqrt(d)) with the rows NOT yet normalised (the first step's
+    renormalisation of every row, ~18 keys per row, lists at their bench
+    capacities) -- vs the float64 oracle, chunked by 128 positives, at the
+    same 1e-5 bar as every other case."""
+    from KGE import loss, score
+    X, E, R = _fb15k237()
+    rng = np.random.default_rng(1024 + (idx == torch.int32))
+    pos = X[rng.choice(len(X), 1024, replace=False)]
+    lim = 6.0 / np.sqrt(200)
+    W = {"ent_emb": rng.uniform(-lim, lim, (E, 200)).astype(np.float32),
+         "rel_emb": rng.uniform(-lim, lim, (R, 200)).astype(np.float32)}
+    ref, got, l_, ps, ns, _, neg = run_case(hiplib, "TransE", 200, 1024, 256, "h+t", score.LpDistance(2),
+                                            loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E=E, R=R, pos=pos,
+                                            W=W, lr=0.01, idx=idx, oracle_chunk=128)
+    assert len(np.unique(neg)) > 0.99 * E   # (every row has a gradient: ~18 draws per row)
+    check(ref, got, l_, ps, ns)
+
+
+def test_rotate_c3_full_size(hiplib):
+    """C3 exactly as the bench times it (BASELINE configs[2]; RotatE.py:126-165):
+    RotatE d = 256 complex, B = 1024 real FB15k-237 positives, K = 256 'h+t',
+    LpDistance(1), SANS(3, 1), SGD lr 0.01, E = 14,505, R = 237, weights in the
+    reference initialiser's range U(+-(gamma + 2) / d) -- vs the float64
+    oracle, chunked by 128 positives, at the 1e-5 bar."""
+    from KGE import loss, score
+    X, E, R = _fb15k237()
+    rng = np.random.default_rng(256)
+    pos = X[rng.choice(len(X), 1024, replace=False)]
+    lim = 5.0 / 256
+    W = {"ent_emb": rng.uniform(-lim, lim, (E, 256, 2)).astype(np.float32),
+         "rel_emb": rng.uniform(-lim, lim, (R, 256)).astype(np.float32)}
+    ref, got, l_, ps, ns, _, _ = run_case(hiplib, "RotatE", 256, 1024, 256, "h+t", score.LpDistance(1),
+                                          loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0), E=E, R=R, pos=pos,
+                                          W=W, lr=0.01, oracle_chunk=128)
+    check(ref, got, l_, ps, ns)
 
 
 @pytest.mark.parametrize("model_name", ["TransE", "DistMult", "RotatE"])
@@ -1108,12 +1218,12 @@ def test_gathered_shard_layout_remap(hiplib, model_name):
         np.testing.assert_allclose(got, v, atol=TOL, err_msg=kk)
 
 
-@pytest.mark.parametrize("loopback", [False, True])
-def test_sharded_step_c5_shard_size(hiplib, loopback):
+@pytest.mark.parametrize("mode,loopback", [("sparse", False), ("sparse", True), ("owner", False), ("owner", True)])
+def test_sharded_step_c5_shard_size(hiplib, mode, loopback):
     """One GPU at the C5 per-rank shard size (6.25M rows x 512, TransE, K=256
-    h+t, SANS) through the sparse exchange: finite loss, only touched rows
-    change, and the owner update equals the fused single-device step on the
-    same rows (same draws)."""
+    h+t, SANS) through the sparse exchange or owner-side scoring (the mode
+    "auto" gives C5): finite loss, only touched rows change, and the sharded
+    step equals the fused single-device step on the same rows (same draws)."""
     import torch.distributed as dist
     from KGE import engine, loss, optimizers, score
     from KGE.ns_strategy import UniformStrategy
@@ -1133,7 +1243,7 @@ def test_sharded_step_c5_shard_size(hiplib, loopback):
             m = _make("TransE", d, K, "h+t", score.LpDistance(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
                       E, R, UniformStrategy(np.arange(E), seed=5), constraint=False)
             m.model_weights = {"ent_emb": ent.clone(), "rel_emb": rel.clone()}
-            stp = ShardedStep(m, mode="sparse", local_fast=False, loopback=loopback) if sharded else \
+            stp = ShardedStep(m, mode=mode, local_fast=False, loopback=loopback) if sharded else \
                 engine.FusedStep(m)
             lv = float(stp(pos, True, optimizers.SGD(0.01)))
             torch.cuda.synchronize()
@@ -1217,5 +1327,90 @@ def test_owner_merge_hot_entities(hiplib, loopback):
             del st
         for kk in outs[0]:   # (rel_seg adds four row groups' partials: equal up to summation order)
             np.testing.assert_allclose(outs[0][kk], outs[1][kk], rtol=0, atol=1e-6, err_msg=kk)
+    finally:
+        dist.destroy_process_group()
+
+
+def _zipf(rng, n, N, s):
+    """Truncated power-law ranks in [1, N] (inverse CDF of the continuous
+    Zipf(s) density) scattered over the id space by k -> (a (k-1) + b) mod N
+    (the C5 generator of bench.py)."""
+    u = rng.random(n)
+    k = np.clip(np.floor((1.0 + u * (float(N) ** (1.0 - s) - 1.0)) ** (1.0 / (1.0 - s))), 1, N).astype(np.int64)
+    a = 2654435761
+    while np.gcd(a, N) != 1:
+        a += 2
+    return (a * (k - 1) + 40503) % N
+
+
+def _touched_rows_oracle(ent, rel, steps, lr, chunk):
+    """The oracle on the rows the steps touch (SGD, no constraint: nothing in
+    the step reads an untouched row, TransE.py:127-174 / loss.py:174-182):
+    ids renumbered into a compact table, ``train_step_chunked`` step after
+    step. Returns (touched ids, updated rows, losses)."""
+    ids = np.unique(np.concatenate([np.concatenate([p[:, 0], p[:, 2], n]) for p, n in steps]))
+    W = {"ent_emb": ent[torch.as_tensor(ids, device=ent.device)].cpu().numpy(), "rel_emb": rel.cpu().numpy()}
+    losses = []
+    for p, n in steps:
+        pp = p.copy()
+        pp[:, 0] = np.searchsorted(ids, p[:, 0])
+        pp[:, 2] = np.searchsorted(ids, p[:, 2])
+        ref = orc.train_step_chunked("TransE", W, pp, np.searchsorted(ids, n), score=("lp", 2.0),
+                                     loss=("sans", 3.0, 1.0), lr=lr, constraint=False, chunk=chunk)
+        W = ref["weights"]
+        losses.append(ref["loss"])
+    return ids, W, losses
+
+
+@pytest.mark.parametrize("loopback", [False, True])
+def test_owner_c5_kernel_shape(hiplib, loopback):
+    """Owner-side scoring (what "auto" runs for C5) at C5's kernel shape:
+    TransE d = 512 (two fragment chunks per row), K = 256 'h+t' (four waves per
+    positive: each owner record merges the waves' partial softmax states,
+    then the merge combines the records), E = 2M rows (compact launches),
+    Zipf(1.1) heads / tails and Zipf(1.2) relations over R = 1000 (hot rows:
+    long_rows_kernel, rel_seg_kernel), SANS(3, 1), SGD; world-1 RCCL, with
+    and without every positive row through the exchange blocks. Two steps ==
+    two float64 oracle steps on the touched rows (TransE.py:127-174,
+    loss.py:174-182) at the 1e-5 bar; every other row bit-unchanged."""
+    import torch.distributed as dist
+    from KGE import loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    from KGE.sharded import ShardedStep
+    dev = _dev()
+    _init_world1(dist, dev)
+    try:
+        E, R, d, B, K = 2_000_000, 1000, 512, 512, 256
+        g = torch.Generator(device=dev).manual_seed(5)
+        lim = 6.0 / math.sqrt(d)
+        ent0 = torch.rand(E, d, generator=g, device=dev).mul_(2).sub_(1).mul_(lim)
+        rel0 = torch.rand(R, d, generator=g, device=dev).mul_(2).sub_(1).mul_(lim)
+        rng = np.random.default_rng(55 + loopback)
+        m = _make("TransE", d, K, "h+t", score.LpDistance(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
+                  E, R, UniformStrategy(np.arange(E), seed=6), constraint=False)
+        m.model_weights = {"ent_emb": ent0.clone(), "rel_emb": rel0.clone()}
+        st = ShardedStep(m, mode="owner", loopback=loopback, local_fast=False, batch_hint=B)
+        assert st.mode == "owner"
+        opt = optimizers.SGD(0.05)
+        steps, got_losses = [], []
+        for _ in range(2):
+            pos = np.stack([_zipf(rng, B, E, 1.1), _zipf(rng, B, R, 1.2), _zipf(rng, B, E, 1.1)], 1)
+            plane = m.ns_strategy.offset
+            got_losses.append(float(st(torch.tensor(pos, device=dev), True, opt)))
+            torch.cuda.synchronize()
+            st.check_status()
+            steps.append((pos, orc.negatives(pos, K, "h+t", E, seed=6, plane=plane)))
+        assert np.bincount(steps[0][0][:, 0]).max() >= 16   # (a Zipf-hot head)
+        st.sync()
+        ids, ref_w, ref_losses = _touched_rows_oracle(ent0, rel0, steps, 0.05, 64)
+        for it, (a, b) in enumerate(zip(got_losses, ref_losses)):
+            assert abs(a - b) <= TOL * max(1.0, abs(b)), (it, a, b)
+        got = m.model_weights["ent_emb"]
+        tid = torch.as_tensor(ids, device=dev)
+        np.testing.assert_allclose(got[tid].cpu().numpy(), ref_w["ent_emb"], rtol=0, atol=TOL, err_msg="ent_emb")
+        np.testing.assert_allclose(m.model_weights["rel_emb"].cpu().numpy(), ref_w["rel_emb"], rtol=0, atol=TOL,
+                                   err_msg="rel_emb")
+        changed = torch.nonzero((got != ent0).any(dim=1)).flatten().cpu().numpy()
+        assert np.isin(changed, ids).all()
     finally:
         dist.destroy_process_group()

@@ -92,12 +92,20 @@ def _worker(rank, port, name, loss, opt, steps, mode, out):
     from KGE.sharded import ShardedStep
     W, pos, neg = _case(0, name)
     m = _model(name, W, loss)
-    st = ShardedStep(m, mode=mode)
+    o = optimizers.SGD(0.05) if opt == "sgd" else optimizers.Adam(0.01)
+    if mode == "auto-large":
+        # "auto" on a table past the dense threshold, told the optimizer (as
+        # KGEModel.train does): owner-side scoring only for SGD steps
+        import KGE.sharded as S
+        S.DENSE_TABLE_BYTES = 0
+        st = ShardedStep(m, optimizer=o)
+        mode = "owner" if opt == "sgd" and name in ("TransE", "DistMult", "RotatE") else "sparse"
+    else:
+        st = ShardedStep(m, mode=mode)
     assert st.valid == len(range(rank, E, 2))
     if mode == "dense":
         assert not hasattr(st, "shard") and len(st.gent) == (2 if name == "TransD" else 1)
     assert st.mode == mode
-    o = optimizers.SGD(0.05) if opt == "sgd" else optimizers.Adam(0.01)
     for s in range(steps):
         b = torch.tensor(pos[rank * B:(rank + 1) * B])
         n = torch.tensor(neg[rank * B * K:(rank + 1) * B * K])
@@ -188,9 +196,11 @@ def test_sparse_mode_refuses_full_table_regulariser():
         os.environ.pop("KGE_BACKEND", None)
 
 
-@pytest.mark.parametrize("mode", ["sparse", "dense"])
+@pytest.mark.parametrize("mode", ["sparse", "dense", "auto-large"])
 def test_sharded_adam_equals_single_device_eager(mode):
-    """Two Adam steps across 2 ranks == two steps of the single-process eager path at 2B."""
+    """Two Adam steps across 2 ranks == two steps of the single-process eager
+    path at 2B ("auto-large": "auto" above the dense threshold with keras Adam
+    takes the row exchange, not owner-side scoring)."""
     os.environ["KGE_BACKEND"] = "eager"
     try:
         from KGE import engine, optimizers
@@ -205,3 +215,30 @@ def test_sharded_adam_equals_single_device_eager(mode):
         os.environ.pop("KGE_BACKEND", None)
     for k, v in m.model_weights.items():
         np.testing.assert_allclose(got[k], v.numpy(), atol=2e-6, err_msg=k)
+
+
+def test_auto_mode_follows_the_optimizer():
+    """ShardedStep "auto" above the dense-table threshold: owner-side scoring
+    for TransE / DistMult / RotatE with SGD (or an unknown optimizer), the
+    row exchange for keras Adam and for the other models."""
+    os.environ["KGE_BACKEND"] = "eager"
+    try:
+        import torch.distributed as dist
+        import KGE.sharded as S
+        from KGE import optimizers
+        dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % _port(), rank=0, world_size=1)
+        old = S.DENSE_TABLE_BYTES
+        S.DENSE_TABLE_BYTES = 0
+        try:
+            W, _, _ = _case(0, "TransE")
+            m = _model("TransE", W, "sans")
+            assert S.ShardedStep(m, optimizer=optimizers.SGD(0.1)).mode == "owner"
+            assert S.ShardedStep(m, optimizer=optimizers.Adam(0.01)).mode == "sparse"
+            assert S.ShardedStep(m).mode == "owner"
+            W, _, _ = _case(0, "TransD")
+            assert S.ShardedStep(_model("TransD", W, "hinge"), optimizer=optimizers.SGD(0.1)).mode == "sparse"
+        finally:
+            S.DENSE_TABLE_BYTES = old
+            dist.destroy_process_group()
+    finally:
+        os.environ.pop("KGE_BACKEND", None)
