@@ -471,9 +471,10 @@ kge_status kge_stream_batch_perm(const kge_stream_desc* d, const int32_t* perm_l
 kge_status kge_histogram(const float* x, int64_t n, const double* lo_width, int32_t buckets,
                          unsigned long long* counts, void* stream);
 
-/* Device copy of n16 16-byte elements, src -> dst (non-overlapping, both
- * 16-byte aligned): each lane moves four float4s, every load issued before any
- * store. A plain streaming copy: bench.py times it on a buffer far larger than
+/* Device copy of n16 16-byte elements (n16 <= 2^40), src -> dst
+ * (non-overlapping, both 16-byte aligned): one pass, each workgroup a
+ * contiguous 16 KiB, non-temporal loads and stores, every load issued before
+ * any store. A streaming copy: bench.py times it on a buffer far larger than
  * the Infinity Cache as the box's measured HBM copy peak, the second
  * denominator of the step's roofline fraction. */
 kge_status kge_copy16(const void* src, void* dst, int64_t n16, void* stream);

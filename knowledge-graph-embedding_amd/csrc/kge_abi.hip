@@ -546,12 +546,16 @@ __global__ __launch_bounds__(256) void phase_gate_kernel(StepCtl* ctl, uint32_t 
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
     zero[q] = 0.f;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const uint32_t s = ctl->plan_sig, p = ctl->score_pending;
-    ctl->score_pending = 0u;
+    // vector (atomic) loads, and the reset only after p is known: plain
+    // loads of these uniform words become scalar loads, which the reset's
+    // vector store may overtake (it would read its own 0)
+    const uint32_t s = __hip_atomic_load(&ctl->plan_sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t p = __hip_atomic_load(&ctl->score_pending, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (p != 0u) __hip_atomic_store(&ctl->score_pending, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (s != sig || p != sig) {
       // (s is another plan's: its kernels refuse the workspace anyway; 0: the
       // update pass would claim a fresh workspace and run on empty lists)
-      if (s == 0u || s == sig) ctl->plan_sig = kPoisonedSig;
+      if (s == 0u || s == sig) __hip_atomic_store(&ctl->plan_sig, kPoisonedSig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       set_status(status, KGE_EWORKSPACE);
     }
   }
@@ -711,7 +715,7 @@ kge_status kge_histogram(const float* x, int64_t n, const double* lo_width, int3
 }
 
 kge_status kge_copy16(const void* src, void* dst, int64_t n16, void* stream) {
-  if (n16 < 0) return fail(KGE_EINVAL, "kge_copy16: n16 must be >= 0");
+  if (n16 < 0 || n16 > ((int64_t)1 << 40)) return fail(KGE_EINVAL, "kge_copy16: n16 must be in [0, 2^40]");
   if (n16 == 0) return KGE_OK;
   if (!src || !dst || ((uintptr_t)src | (uintptr_t)dst) & 15)
     return fail(KGE_EINVAL, "kge_copy16: null or unaligned src / dst");

@@ -131,24 +131,28 @@ void launch_histogram(const float* x, int64_t n, const double* lw, int bc, unsig
   hipLaunchKernelGGL(histogram_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, lw, bc, counts);
 }
 
-// ---- kge_copy16: the streaming copy bench.py measures the HBM peak with
-__global__ __launch_bounds__(256) void copy16_kernel(const float4* __restrict__ src, float4* __restrict__ dst,
+// ---- kge_copy16: the streaming copy bench.py measures the HBM peak with.
+// One pass, no grid-stride loop: workgroup b copies the contiguous 16 KiB
+// [b * 1024, (b + 1) * 1024) float4s, each lane four of them 4 KiB apart,
+// every load issued before any store, non-temporal both ways (the fastest of
+// the variants tools/copy_peak.hip measures: 6.2 TB/s vs 4.5-5.4 for
+// grid-stride loops and 4.9 for hipMemcpy, profiles/r05c/copy_peak.txt)
+typedef float kge_v4f __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void copy16_kernel(const kge_v4f* __restrict__ src, kge_v4f* __restrict__ dst,
                                                      int64_t n) {
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += 4 * stride) {
-    float4 v[4];
+  const int64_t base = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  kge_v4f v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (i + u * stride < n) v[u] = src[i + u * stride];
+  for (int u = 0; u < 4; ++u)
+    if (base + u * 256 < n) v[u] = __builtin_nontemporal_load(src + base + u * 256);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (i + u * stride < n) dst[i + u * stride] = v[u];
-  }
+  for (int u = 0; u < 4; ++u)
+    if (base + u * 256 < n) __builtin_nontemporal_store(v[u], dst + base + u * 256);
 }
 
 void launch_copy16(const void* src, void* dst, int64_t n16, hipStream_t st) {
-  const int64_t blocks = std::min<int64_t>(std::max<int64_t>((n16 + 1023) / 1024, 1), 256 * 32);
-  hipLaunchKernelGGL(copy16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const float4*)src, (float4*)dst,
+  const int64_t blocks = (n16 + 1023) / 1024;   // (kge_copy16 caps n16 at 2^40)
+  hipLaunchKernelGGL(copy16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const kge_v4f*)src, (kge_v4f*)dst,
                      n16);
 }
 
