@@ -347,8 +347,8 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   const bool active = grp < nValid;
   const int64_t i = i0 + grp;
   const MP mp{A.limit, A.fuse_norm, A.snap + (active ? i : 0) * (M::NSNAP * (int64_t)A.snap_cols)};
-  int jbeg = min(Keff, gw * A.SW);
-  int jend = min(Keff, jbeg + A.SW);
+  const int jbeg = min(Keff, gw * A.SW);
+  const int jend = min(Keff, jbeg + A.SW);
   int32_t* ids = s_ids + grp * Keff;
   float* gR = s_R + grp * Keff;
   float* gT = s_T + grp * Keff;
@@ -431,8 +431,6 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
       hb = min(nh, gw * swh); he = min(nh, hb + swh);
       tb = nh + min(nt, gw * swt); te = nh + min(nt, gw * swt + swt);
     }
-    jbeg = hb;
-    jend = te;
   }
   KGE_PROF(0);
 
@@ -508,10 +506,11 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
     // (NRM_FROM_R models: lanes past the row's end keep whatever they
     // loaded and only their score partial is masked -- their accumulator
     // lanes are never read back)
-    auto issue = [&](F (&dst)[ROWS], int jb) {
-      if (((jb - jbeg) & (KGE_WAVE - 1)) == 0) idv = (jb + lane < jend) ? ids[jb + lane] : 0;
-      const int jo = (jb - jbeg) & (KGE_WAVE - 1);
-      const int nr = min(ROWS, jend - jb);
+    // (the stream's range [sb, se) comes in by value: one range per call)
+    auto issue = [&](F (&dst)[ROWS], int jb, const int sb, const int se) {
+      if (((jb - sb) & (KGE_WAVE - 1)) == 0) idv = (jb + lane < se) ? ids[jb + lane] : 0;
+      const int jo = (jb - sb) & (KGE_WAVE - 1);
+      const int nr = min(ROWS, se - jb);
 #pragma unroll
       for (int u = 0; u < ROWS; ++u) {
         const float* row = A.ent.row(__builtin_amdgcn_readlane(idv, jo + min(u, nr - 1)));
@@ -521,21 +520,25 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
     };
     // KGE_SCORE_PREFETCH: the next batch's rows are in flight while this
     // batch is reduced and differentiated (one more batch of registers)
-    // one range [jbeg, jend) of slots whose corruption kinds follow the
-    // pattern S2 (the launch's side; the owner pass: one side per range)
-    auto stream = [&](auto sidec) {
+    // one range [sb, se) of slots whose corruption kinds follow the
+    // pattern S2 (the launch's side; the owner pass: one side per range).
+    // LK: the loss kind when known at compile time (SANS, the configs' loss:
+    // its loop carries no branch of the other kinds), else -1 (A.loss_kind)
+    auto stream = [&](auto sidec, auto lkc, const int sb, const int se) {
     constexpr int S2 = decltype(sidec)::value;
+    constexpr int LK = decltype(lkc)::value;
+    const int lk = LK >= 0 ? LK : A.loss_kind;
     F En[KGE_SCORE_PREFETCH ? ROWS : 1];
-    if constexpr (KGE_SCORE_PREFETCH) issue(En, jbeg);
-    for (int j0 = jbeg; j0 < jend; j0 += ROWS) {
-      const int nrow = min(ROWS, jend - j0);   // wave-uniform, >= 1
+    if constexpr (KGE_SCORE_PREFETCH) issue(En, sb, sb, se);
+    for (int j0 = sb; j0 < se; j0 += ROWS) {
+      const int nrow = min(ROWS, se - j0);   // wave-uniform, >= 1
       F E[ROWS];
       if constexpr (KGE_SCORE_PREFETCH) {
 #pragma unroll
         for (int u = 0; u < ROWS; ++u) E[u] = En[u];
-        if (j0 + ROWS < jend) issue(En, j0 + ROWS);
+        if (j0 + ROWS < se) issue(En, j0 + ROWS, sb, se);
       } else {
-        issue(E, j0);
+        issue(E, j0, sb, se);
       }
       if (A.fuse_norm) {
         // fused _constraint_loss: each sampled row normalised in registers
@@ -572,7 +575,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
       float lp;
       const float s = score_value_fast<SK>(Rl, A.pw, &lp, A.p);
       float c = 0.f;
-      switch (A.loss_kind) {
+      switch (lk) {
         case KGE_LOSS_HINGE: {
           // the hinge's on/off decision is the finalise pass's (IEEE score), so
           // a negative on the margin is active for its own row and for its
@@ -630,15 +633,15 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
       });
     }
     };
+    auto stream_lk = [&](auto sidec, const int sb, const int se) {
+      if (A.loss_kind == KGE_LOSS_SANS) stream(sidec, std::integral_constant<int, KGE_LOSS_SANS>{}, sb, se);
+      else stream(sidec, std::integral_constant<int, -1>{}, sb, se);
+    };
     if constexpr (OWN) {
-      jbeg = hb; jend = he;
-      stream(std::integral_constant<int, SIDE == KGE_SIDE_HT ? KGE_SIDE_H : SIDE>{});
-      if constexpr (SIDE == KGE_SIDE_HT) {
-        jbeg = tb; jend = te;
-        stream(std::integral_constant<int, KGE_SIDE_T>{});
-      }
+      stream_lk(std::integral_constant<int, SIDE == KGE_SIDE_HT ? KGE_SIDE_H : SIDE>{}, hb, he);
+      if constexpr (SIDE == KGE_SIDE_HT) stream_lk(std::integral_constant<int, KGE_SIDE_T>{}, tb, te);
     } else {
-      stream(std::integral_constant<int, SIDE>{});
+      stream_lk(std::integral_constant<int, SIDE>{}, jbeg, jend);
     }
     M::finish(accH, accR, accT);
   }
