@@ -15,7 +15,8 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = ("score_kernel", "update_kernel", "constrain_rows_kernel", "apply_kernel")
+KERNELS = ("score_kernel", "update_kernel", "constrain_rows_kernel", "apply_kernel", "rel_item_kernel", "rel_dr_kernel",
+           "rescal_apply_kernel", "transr_kernel", "transr_proj_apply")
 
 
 def short(name):
