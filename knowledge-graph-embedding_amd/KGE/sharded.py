@@ -892,8 +892,12 @@ class ShardedStep:
         P = ext[b["pos_base"]:b["pos_base"] + 2 * G * Bn]
         mine = P[2 * g * Bn:2 * (g + 1) * Bn]
         mine.copy_(ext.index_select(0, lpos[:, 0::2].reshape(-1).to(torch.int64)))   # (a view of ext: no out=)
-        ex.all_gather(P, mine)
-        ex.all_gather(o["gtrip"], batch)
+        gtrip = o["gtrip"]
+        if G > 1:   # (one rank: P is `mine`, the virtual batch is the batch)
+            ex.all_gather(P, mine)
+            ex.all_gather(gtrip, batch)
+        else:
+            gtrip = batch
         if given:
             ex.all_gather(o["gneg"], neg_ids.to(batch.dtype).contiguous())
         else:
@@ -908,7 +912,7 @@ class ShardedStep:
         fo, fm = o["fo"], o["fm"]
         fo.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER | _hip.FLAG_PHASE_SCORE
         opt = optimizer if is_train else None
-        fo(o["gtrip"], is_train, opt, neg_ids=o["gneg"], prof_events=ev_s)
+        fo(gtrip, is_train, opt, neg_ids=o["gneg"], prof_events=ev_s)
         # 4. records to the positives' ranks; 5. merge
         if G > 1:
             ex.all_to_all(o["rec_in"], o["rec"])
@@ -926,7 +930,7 @@ class ShardedStep:
         # 7. the owned negatives' rows, then 8. the positives' rows
         fo.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER | _hip.FLAG_PHASE_UPDATE
         fo.abort = small[-1:]
-        fo(o["gtrip"], True, optimizer, neg_ids=o["gneg"], prof_events=ev_u)
+        fo(gtrip, True, optimizer, neg_ids=o["gneg"], prof_events=ev_u)
         fm.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER_MERGE | _hip.FLAG_PHASE_UPDATE | self.debug_flags
         fm.abort = small[-1:]
         fm(lpos, True, optimizer)

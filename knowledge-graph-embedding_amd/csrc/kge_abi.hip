@@ -53,7 +53,8 @@ struct Plan {
   int hbits;
   uint64_t o_gnegp, o_gpos2, o_gdense[3], o_dpart;   // TransH / TransD
   uint64_t o_owncodes;                               // owner-side scoring
-  bool rescal, transr, proj, td, pj_dense, own, omerge, pos_only;
+  uint64_t o_segraw, o_segkeys, o_segpart;           // owner merge update: segmented sum
+  bool rescal, transr, proj, td, pj_dense, own, omerge, pos_only, seg;
   uint32_t lng_cap;
   uint32_t sig;   // workspace plan signature
 };
@@ -361,7 +362,19 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   // the owner merge's update pass (compact): relation rows by rel_seg_kernel.
   // Not in the other compact launches: there the update kernel's hot-relation
   // waves overlap its ~10^5 other waves, and the extra launch cost C5 24 us
-  A.rel_seg = compact && omerge && !(d->flags & KGE_FLAG_DEBUG_NO_REL_SEG);
+  // the owner merge's SGD update pass as a segmented sum over the positives'
+  // keys (launch_merge_segsum): no update kernel / rel_rank / rel_seg /
+  // long_rows chain. (KGE_FLAG_DEBUG_NO_REL_SEG keeps the update kernel
+  // summing every destination, for A-B tests.)
+  int seg_npad = 64;
+  if (3 * B > kSegMaxKeys) seg_npad = 2 * kSegMaxKeys;   // (too many keys for one workgroup's sort)
+  while (seg_npad < 3 * B) seg_npad <<= 1;
+  const bool seg_merge = omerge && d->optimizer == KGE_OPT_SGD && seg_npad <= kSegMaxKeys && rowlen <= 1024 &&
+                         entc % 4 == 0 && rowlen % 4 == 0 && (rescal ? entc : relc) % 4 == 0 &&
+                         !(d->flags & KGE_FLAG_DEBUG_NO_REL_SEG);
+  A.seg_merge = seg_merge;
+  A.seg_npad = seg_npad;
+  A.rel_seg = compact && omerge && !seg_merge && !(d->flags & KGE_FLAG_DEBUG_NO_REL_SEG);
   A.dense = rescal && A.train;
   A.dense_ent = rescal ? (float)(2.0 * d->constraint_weight / (double)E) : 0.f;
   A.lr = d->lr;
@@ -475,14 +488,21 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     }
   }
   if (own) P.o_owncodes = take((uint64_t)T * 4);
-  const bool rel_seg = compact && omerge && !(d->flags & KGE_FLAG_DEBUG_NO_REL_SEG);
+  const bool rel_seg = A.rel_seg;
   if (rel_seg) {   // launch_rel_rank's output for rel_seg_kernel
     P.o_rsorted = take((uint64_t)B * 4);
     P.o_rsrel = take((uint64_t)B * 4);
     P.o_rsbeg = take((uint64_t)R * 2 * 4);
   }
   // owner merge, SGD update pass: long destination lists deferred (kLongN)
-  const bool pos_only = omerge && compact && d->optimizer == KGE_OPT_SGD && !fuse_norm_plan && entc <= 256 * kLongCPT;
+  const bool pos_only = omerge && compact && !seg_merge && d->optimizer == KGE_OPT_SGD && !fuse_norm_plan &&
+                        entc <= 256 * kLongCPT;
+  P.seg = seg_merge;
+  if (seg_merge) {
+    P.o_segraw = take((uint64_t)3 * B * 8);
+    P.o_segkeys = take((uint64_t)3 * B * 8);
+    P.o_segpart = take((uint64_t)2 * ceil_div(3 * B, 4) * rowlen * 4);   // (chunks of >= 4 keys)
+  }
   const uint32_t lng_cap = (uint32_t)(T / kLongN + 1);
   if (pos_only) P.o_lng = take((uint64_t)lng_cap * 16);
   P.pos_only = pos_only;
@@ -498,7 +518,8 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
                          (int64_t)P.o_cnt, (int64_t)P.o_htab, (int64_t)P.o_coef, (int64_t)P.o_snap,
                          (int64_t)P.o_gpos, (int64_t)P.o_part, (int64_t)P.o_list, (int64_t)P.o_ovf,
                          (int64_t)P.o_upart, (int64_t)P.o_leaders, (int64_t)P.o_sorted, (int64_t)P.o_relseg,
-                         (int64_t)P.o_gneg, (int64_t)P.o_dpart, (int64_t)P.o_owncodes, T,
+                         (int64_t)P.o_gneg, (int64_t)P.o_dpart, (int64_t)P.o_owncodes, (int64_t)P.o_segraw, (int64_t)P.o_segkeys,
+                         (int64_t)P.o_segpart, T,
                          (int64_t)d->owner_world, (int64_t)d->owner_batch};
     uint32_t h = 2166136261u;
     for (const int64_t v : f)
@@ -783,6 +804,11 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     A.lng = (uint4*)(ws + P.o_lng);
     A.lng_cap = P.lng_cap;
   }
+  if (P.seg) {
+    A.seg_raw = (unsigned long long*)(ws + P.o_segraw);
+    A.seg_keys = (unsigned long long*)(ws + P.o_segkeys);
+    A.seg_part = (float*)(ws + P.o_segpart);
+  }
   if (P.own || P.omerge) {
     // owner-side scoring: OWNER | SCORE (owner pass), OWNER | UPDATE
     // (coefficients + the owned rows' update), OWNER_MERGE | SCORE (merge),
@@ -793,7 +819,7 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     if (d->batch > 0) {
       // the phase gate; the merge's relation gradients start from zero
       // (rel_seg writes every row's every column itself)
-      if (upd) {
+      if (upd && !(P.omerge && P.seg)) {   // (the segmented merge update gates itself)
         const bool zero = P.omerge && !(A.rel_seg && A.rel_gcols == A.rel.cols);
         launch_phase_gate(A.ctl, A.sig, A.status, zero ? d->grad_out[1] : nullptr,
                           zero ? A.rel.rows * (int64_t)A.rel_gcols : 0, st);
@@ -805,7 +831,9 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
         if (s != KGE_OK) return fail(s, "no owner-pass instance for model %d / score %d", d->model, P.sk);
       }
       if (ev && !upd) (void)hipEventRecord(ev[2], st);
-      if (upd) {
+      if (upd && P.omerge && P.seg) {
+        launch_merge_segsum(A, st);
+      } else if (upd) {
         A.run_score = false;
         s = launch_step_elementwise(A, P.G, d->model, P.sk, st, ev);
         if (s != KGE_OK) return fail(s, "no kernel instance for model %d / score %d", d->model, P.sk);

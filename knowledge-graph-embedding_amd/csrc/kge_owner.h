@@ -187,7 +187,12 @@ __global__ __launch_bounds__(kMergeWaves * KGE_WAVE) void owner_merge_kernel(Ste
           A.gpos[i * 3 * (int64_t)A.gcols + v * (int64_t)A.gcols + k] = s;
         }
       }
-      if (lane < 3 && (A.rel_dests || lane != 2)) {
+      if (A.seg_merge) {   // the segmented update pass's keys: (destination << 32 | 4 i + c)
+        if (lane < 3) {
+          const int64_t dest = lane == 0 ? ph : lane == 1 ? pt : A.ent.rows + pr;
+          A.seg_raw[3 * i + lane] = ((unsigned long long)dest << 32) | (unsigned long long)(4u * (uint32_t)i + lane);
+        }
+      } else if (lane < 3 && (A.rel_dests || lane != 2)) {
         const int64_t dest = lane == 0 ? ph : lane == 1 ? pt : A.ent.rows + pr;
         bin_key(A, dest, A.nkeyneg + (((uint32_t)i) << 2) + (uint32_t)lane);
       }

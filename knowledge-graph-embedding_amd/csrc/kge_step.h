@@ -197,6 +197,17 @@ struct StepArgs {
   bool pos_only = false;
   uint4* lng = nullptr;
   uint32_t lng_cap = 0;
+  // merge update as a segmented sum (launch_merge_segsum, kge_step.hip): the
+  // positives' 3 B keys (destination, code) sorted once, summed in chunks of
+  // 4-16 keys by many waves (a Zipf-hot destination is split over
+  // chunks, no serial chain), chunk-spanning runs combined in chunk order.
+  // Replaces the update kernel, rel_rank, rel_seg and long_rows of the merge's
+  // update pass; the merge files no keys
+  bool seg_merge = false;
+  unsigned long long* seg_raw = nullptr;    // [3 B] the merge's keys (destination << 32 | code), positive order
+  unsigned long long* seg_keys = nullptr;   // [3 B] the same, sorted
+  float* seg_part = nullptr;                // [2 * chunks, gcols] head / tail partial rows
+  int32_t seg_npad = 0;                     // (a power of two >= 3 B, <= kSegMaxKeys: the key staging bound)
   // entity ids -> table rows: n_ent global ids; rG > 1: the table is G
   // all-gathered shards of rEs rows, id e at (e mod rG) * rEs + e div rG
   int64_t n_ent = 0;
@@ -309,6 +320,10 @@ void launch_rel_rank(const RelArgs& R, hipStream_t st);
 void launch_histogram(const float* x, int64_t n, const double* lw, int bc, unsigned long long* counts,
                       hipStream_t st);   // kge_stream.hip (kge_histogram)
 void launch_copy16(const void* src, void* dst, int64_t n16, hipStream_t st);   // kge_stream.hip (kge_copy16)
+constexpr int kSegMaxKeys = 8192;
+// the owner merge's update pass (StepArgs::seg_merge): phase gate + relation
+// gradient zero-fill + key sort, chunk sums, combine (kge_step.hip)
+void launch_merge_segsum(const StepArgs& A, hipStream_t st);
 void launch_rel_post(const RelArgs& R, hipStream_t st);     // dR (+ dense term, norm^2 partials)
 // train step tail: both passes' norms + the loss term, then both SGD applies in one launch
 void launch_rescal_norms(const RelArgs& P, const float* upart, int nu, float lam, float lr, float clip,

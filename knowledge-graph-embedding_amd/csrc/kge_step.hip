@@ -195,6 +195,291 @@ void launch_apply_many(const ApplyArgs* a, int n, hipStream_t st) {
 
 void launch_apply(const ApplyArgs& a, hipStream_t st) { launch_apply_many(&a, 1, st); }
 
+// ------------------------------------------------------------ owner merge update
+// The update pass of the owner merge (KGE_FLAG_OWNER_MERGE | PHASE_UPDATE,
+// StepArgs::seg_merge): this rank's positives' own row gradients (gpos rows,
+// owner_merge_kernel) summed per destination -- head / tail entity rows
+// (own rows: the clip-scaled SGD step; fetched rows >= remote_from: the raw
+// gradient in place) and relation rows (raw gradient into grel) -- as a
+// segmented sum over the n = 3 B keys (destination << 32 | code), code = 4 i
+// + c (c: 0 head, 1 tail, 2 relation):
+//   M1  plan     the split-step phase gate (workgroup 0), grel zero-filled,
+//                and every key (written by the merge, seg_raw) placed at its
+//                rank (#smaller keys: the keys are distinct) -- all n keys
+//                staged in each workgroup's LDS, a wave per 4 keys, no sort
+//                passes;
+//   M2  chunks   a wave per CH (4-8) consecutive sorted keys, every gradient row and
+//                destination row of the chunk requested at once; each run of
+//                one destination that starts and ends in the chunk is summed
+//                (ascending code) and applied; a run entering from the
+//                previous chunk leaves a head partial, one leaving into the
+//                next chunk a tail partial;
+//   M3  combine  the wave of the chunk where a chunk-spanning run starts
+//                finds the run's last chunk (64 chunks tested per step), adds
+//                its tail partial and the following chunks' head partials in
+//                chunk order (8 in flight), and applies the sum.
+// A Zipf-hot destination (hundreds of keys at C5) is summed by many waves,
+// not one chain (the update kernel / rel_rank / rel_seg / long_rows sequence
+// this replaces took ~80 us per step there). Same values every run.
+__global__ __launch_bounds__(256) void merge_plan_kernel(StepArgs A, float* zero, int64_t nz) {
+  __shared__ unsigned long long s_k[kSegMaxKeys];
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nz; q += (int64_t)gridDim.x * blockDim.x)
+    zero[q] = 0.f;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // the phase gate (phase_gate_kernel, kge_abi.hip), vector loads first
+    const uint32_t s = __hip_atomic_load(&A.ctl->plan_sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t p = __hip_atomic_load(&A.ctl->score_pending, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (p != 0u) __hip_atomic_store(&A.ctl->score_pending, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s != A.sig || p != A.sig) {
+      if (s == 0u || s == A.sig)
+        __hip_atomic_store(&A.ctl->plan_sig, kPoisonedSig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      set_status(A.status, KGE_EWORKSPACE);
+    }
+  }
+  // the keys the merge left (seg_raw, in positive order), staged whole; each
+  // wave ranks 4 of them, its lanes sweeping n / 64 keys each
+  const int n = 3 * (int)A.B;
+  if ((int64_t)blockIdx.x * 16 >= n) return;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) s_k[j] = A.seg_raw[j];
+  __syncthreads();
+  const int lane = lane_id();
+  const int me0 = (int)blockIdx.x * 16 + wave_id() * 4;
+  unsigned long long k[4];
+  int rank[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    k[q] = me0 + q < n ? s_k[me0 + q] : 0ull;
+    rank[q] = 0;
+  }
+  for (int j = lane; j < n; j += KGE_WAVE) {   // one LDS read, four compares
+    const unsigned long long x = s_k[j];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rank[q] += x < k[q];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) rank[q] += __shfl_xor(rank[q], o, KGE_WAVE);
+    if (lane == q && me0 + q < n) A.seg_keys[rank[q]] = k[q];
+  }
+}
+
+// the apply of one destination's summed row g (this lane's columns 4 lane +
+// 256 u); y: the destination row as loaded with the chunk (own entity rows)
+template <int JM>
+__device__ __forceinline__ void seg_apply(const StepArgs& A, int64_t dest, const float4 (&g)[JM],
+                                          const float4 (&y)[JM], float sce) {
+  const int lane = lane_id();
+  if (dest < A.ent.rows) {
+    float* row = A.ent.row_w(dest);
+    const bool raw = dest >= A.remote_from;
+#pragma unroll
+    for (int u = 0; u < JM; ++u) {
+      const int c = 4 * lane + 256 * u;
+      const float v[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
+      const float w[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (c + e < A.ent.cols) row[c + e] = raw ? v[e] : w[e] + v[e] * sce;
+    }
+  } else {
+    const int64_t r = dest - A.ent.rows;
+    float scr = A.ctl->scale[A.sc_rel_idx];
+    if (A.scale_from_norm2) scr = -A.lr * (A.clip_norm / fmaxf(sqrtf(A.norm2_out[A.sc_rel_idx]), A.clip_norm));
+#pragma unroll
+    for (int u = 0; u < JM; ++u) {
+      const int c = 4 * lane + 256 * u;
+      const float v[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (c + e >= A.rel_gcols) break;
+        if (A.rel_grad || A.grad_mode) A.grel[r * (int64_t)A.rel_gcols + c + e] = v[e];
+        else { float* wp = A.rel.row_w(r) + c + e; *wp = *wp + v[e] * scr; }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ float seg_scale_ent(const StepArgs& A) {
+  float sc = A.ctl->scale[A.sc_ent_idx];
+  if (A.scale_from_norm2) sc = -A.lr * (A.clip_norm / fmaxf(sqrtf(A.norm2_out[A.sc_ent_idx]), A.clip_norm));
+  return sc;
+}
+
+// key's gradient row (gpos [B, 3, gcols]: head, relation, tail) and its
+// destination row (own entity rows only; else entity row 0, unused)
+template <int JM>
+__device__ __forceinline__ void seg_load(const StepArgs& A, unsigned long long key, float4 (&x)[JM],
+                                         float4 (&y)[JM]) {
+  const int lane = lane_id();
+  const uint32_t code = (uint32_t)key;
+  const int64_t dest = (int64_t)(key >> 32);
+  const uint32_t c = code & 3u;
+  const int v = c == 0u ? 0 : c == 1u ? 2 : 1;
+  const int cols = v == 1 ? A.rel_gcols : A.ent.cols;
+  const float* g = A.gpos + (int64_t)(code >> 2) * 3 * A.gcols + (int64_t)v * A.gcols;
+  const float* w = A.ent.row(dest < A.ent.rows && dest < A.remote_from ? dest : 0);
+#pragma unroll
+  for (int u = 0; u < JM; ++u) {
+    const int cc = 4 * lane + 256 * u;
+    x[u] = cc < cols ? *reinterpret_cast<const float4*>(g + cc) : make_float4(0.f, 0.f, 0.f, 0.f);
+    y[u] = cc < A.ent.cols ? *reinterpret_cast<const float4*>(w + cc) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int JM>
+constexpr int seg_chunk() { return JM == 1 ? 8 : 4; }   // keys per chunk (a wave each)
+
+template <int JM>
+__global__ __launch_bounds__(256) void merge_chunk_kernel(StepArgs A) {
+  constexpr int CH = seg_chunk<JM>();
+  if (ws_refused(A.ctl, A.sig, A.status, nullptr)) return;
+  if (A.abort_flag && *A.abort_flag != 0.f) return;
+  const int n = 3 * (int)A.B;
+  const int nch = (n + CH - 1) / CH;
+  const int k = (int)blockIdx.x * 4 + wave_id();
+  if (k >= nch) return;
+  const int lane = lane_id();
+  const int j0 = k * CH, cnt = min(CH, n - j0);
+  // the chunk's keys (lanes 0..CH-1) and its neighbours' (lane 62: previous, 63: next)
+  unsigned long long kv = ~0ull;
+  if (lane < cnt) kv = A.seg_keys[j0 + lane];
+  else if (lane == 62 && j0 > 0) kv = A.seg_keys[j0 - 1];
+  else if (lane == 63 && j0 + cnt < n) kv = A.seg_keys[j0 + cnt];
+  auto key_at = [&](int l) { return (unsigned long long)__shfl((long long)kv, l, KGE_WAVE); };
+  const int64_t dprev = j0 > 0 ? (int64_t)(key_at(62) >> 32) : -1;
+  const int64_t dnext = j0 + cnt < n ? (int64_t)(key_at(63) >> 32) : -1;
+  // every row of the chunk in flight at once
+  float4 x[CH][JM], y[CH][JM];
+  int64_t dst[CH];
+#pragma unroll
+  for (int t = 0; t < CH; ++t) {
+    const unsigned long long kt = key_at(min(t, cnt - 1));
+    dst[t] = (int64_t)(kt >> 32);
+    seg_load<JM>(A, kt, x[t], y[t]);
+  }
+  const float sce = seg_scale_ent(A);
+  float4 acc[JM];
+#pragma unroll
+  for (int u = 0; u < JM; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  bool first = true;   // the current run starts at the chunk's first key
+#pragma unroll
+  for (int t = 0; t < CH; ++t) {
+    if (t < cnt) {
+#pragma unroll
+      for (int u = 0; u < JM; ++u) {
+        acc[u].x += x[t][u].x; acc[u].y += x[t][u].y; acc[u].z += x[t][u].z; acc[u].w += x[t][u].w;
+      }
+      const bool last = t == cnt - 1 || dst[t + 1 < CH ? t + 1 : t] != dst[t];
+      if (last) {   // (uniform)
+        const bool from_prev = first && dst[t] == dprev;
+        const bool to_next = t == cnt - 1 && dst[t] == dnext;
+        if (!from_prev && !to_next) {
+          seg_apply<JM>(A, dst[t], acc, y[t], sce);
+        } else {   // head partial (entered from the previous chunk), else tail partial
+          float* pr = A.seg_part + (int64_t)(2 * k + (from_prev ? 0 : 1)) * A.gcols;
+#pragma unroll
+          for (int u = 0; u < JM; ++u) {
+            const int c = 4 * lane + 256 * u;
+            if (c < A.gcols) *reinterpret_cast<float4*>(pr + c) = acc[u];
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < JM; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        first = false;
+      }
+    }
+  }
+}
+
+template <int JM>
+__global__ __launch_bounds__(256) void merge_combine_kernel(StepArgs A) {
+  constexpr int CH = seg_chunk<JM>();
+  if (ws_refused(A.ctl, A.sig, A.status, nullptr)) return;
+  if (A.abort_flag && *A.abort_flag != 0.f) return;
+  const int n = 3 * (int)A.B;
+  const int nch = (n + CH - 1) / CH;
+  const int k = (int)blockIdx.x * 4 + wave_id();
+  if (k >= nch - 1) return;   // (the last chunk's runs cannot leave it)
+  const int lane = lane_id();
+  const int j0 = k * CH;
+  // this chunk's keys (lanes 0..CH-1), the one before it (lane 62), the next chunk's first (63)
+  unsigned long long kv = ~0ull;
+  if (lane < CH) kv = A.seg_keys[j0 + lane];
+  else if (lane == 62 && j0 > 0) kv = A.seg_keys[j0 - 1];
+  else if (lane == 63) kv = A.seg_keys[j0 + CH];
+  const int64_t dk = (int64_t)(kv >> 32);
+  const int64_t dlast = __shfl(dk, CH - 1, KGE_WAVE);
+  if (__shfl(dk, 63, KGE_WAVE) != dlast) return;   // no run leaves this chunk
+  // the leaving run starts here unless it also entered (then an earlier chunk owns it)
+  const uint64_t same = __ballot(lane < CH && dk == dlast);
+  if (same == ((1ull << CH) - 1ull) && j0 > 0 && __shfl(dk, 62, KGE_WAVE) == dlast) return;
+  // the run's last chunk: the first m > k it does not go through (lanes test
+  // 64 chunks at a time: chunk m full, its last key and the next chunk's
+  // first key still the run's destination)
+  int mend = nch - 1;
+  for (int m0 = k + 1; m0 < nch; m0 += KGE_WAVE) {
+    const int m = m0 + lane;
+    bool through = false;
+    if (m < nch - 1) {
+      const int jm = m * CH;
+      through = (int64_t)(A.seg_keys[jm + CH - 1] >> 32) == dlast && (int64_t)(A.seg_keys[jm + CH] >> 32) == dlast;
+    }
+    const uint64_t stop = __ballot(m < nch && !through);
+    if (stop) { mend = m0 + __builtin_ctzll(stop); break; }
+  }
+  float4 acc[JM], y[JM];
+  const float* pr = A.seg_part + (int64_t)(2 * k + 1) * A.gcols;
+  const float* w = A.ent.row(dlast < A.ent.rows && dlast < A.remote_from ? dlast : 0);
+#pragma unroll
+  for (int u = 0; u < JM; ++u) {
+    const int c = 4 * lane + 256 * u;
+    acc[u] = c < A.gcols ? *reinterpret_cast<const float4*>(pr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    y[u] = c < A.ent.cols ? *reinterpret_cast<const float4*>(w + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // the head partials of chunks k + 1 .. mend in chunk order, 8 in flight
+  for (int m0 = k + 1; m0 <= mend; m0 += 8) {
+    float4 x[8][JM];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float* hp = A.seg_part + (int64_t)(2 * min(m0 + t, mend)) * A.gcols;
+#pragma unroll
+      for (int u = 0; u < JM; ++u) {
+        const int c = 4 * lane + 256 * u;
+        x[t][u] = c < A.gcols ? *reinterpret_cast<const float4*>(hp + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+      if (m0 + t <= mend) {
+#pragma unroll
+        for (int u = 0; u < JM; ++u) {
+          acc[u].x += x[t][u].x; acc[u].y += x[t][u].y; acc[u].z += x[t][u].z; acc[u].w += x[t][u].w;
+        }
+      }
+  }
+  seg_apply<JM>(A, dlast, acc, y, seg_scale_ent(A));
+}
+
+template <int JM>
+static void launch_merge_chunks(const StepArgs& A, int n, hipStream_t st) {
+  const int nch = (n + seg_chunk<JM>() - 1) / seg_chunk<JM>();
+  const unsigned g = (unsigned)((nch + 3) / 4);
+  hipLaunchKernelGGL(merge_chunk_kernel<JM>, dim3(g), dim3(256), 0, st, A);
+  hipLaunchKernelGGL(merge_combine_kernel<JM>, dim3(g), dim3(256), 0, st, A);
+}
+
+void launch_merge_segsum(const StepArgs& A, hipStream_t st) {
+  const int64_t nz = (A.rel_grad || A.grad_mode) ? A.rel.rows * (int64_t)A.rel_gcols : 0;
+  const int n = 3 * (int)A.B;
+  const int64_t blocks = std::max<int64_t>({(int64_t)1, (n + 15) / 16, std::min<int64_t>((nz + 1023) / 1024, 256)});
+  hipLaunchKernelGGL(merge_plan_kernel, dim3((unsigned)blocks), dim3(256), 0, st, A, A.grel, nz);
+  const int w = std::max<int>(A.ent.cols, A.rel_gcols);
+  if (w <= 256) launch_merge_chunks<1>(A, n, st);
+  else if (w <= 512) launch_merge_chunks<2>(A, n, st);
+  else launch_merge_chunks<4>(A, n, st);
+}
+
 kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int model, int sk,
                                    hipStream_t st, hipEvent_t const* ev) {
 #ifdef KGE_ONLY_ONE
