@@ -27,74 +27,16 @@
 // The update pass is the shared destination-major kernel in its
 // materialised mode (gradient rows summed in code order); rel_proj is
 // updated by transr_proj_apply.
-#include "kge_step_impl.h"
+#include "kge_transr2.h"
 
 namespace kge {
 
-using f32x4 = __attribute__((ext_vector_type(4))) float;
-
-__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-constexpr int kTrQ = (kTrMaxSlots + kTrWaves - 1) / kTrWaves;   // slots per wave
-constexpr int kTrKV = kTrMaxDim / KGE_WAVE;                     // projected-row floats per lane
-constexpr int kTrKS3 = ((kTrMaxSlots + 1 + 15) / 16) * 4;       // GEMM3 k-steps (K + 2 slot rows, 16-padded)
-
-// element gradient of the score wrt a = x - y (Lp kinds): score_grad's rule
-template <int SK>
-__device__ __forceinline__ float lp_elem_grad(float a, float alpha, float M) {
-  if (SK == SK_P2) return alpha * a;
-  float s = a > 0.f ? alpha : (a < 0.f ? -alpha : 0.f);
-  if (SK == SK_PGEN) return a != 0.f ? s * powf(fabsf(a), M - 1.f) : 0.f;   // M carries p
-  if (SK == SK_PINF && fabsf(a) != M) s = 0.f;
-  return s;
-}
-
-// all-lane sum / max over the wave (permlane + DPP tree, kge_common.h)
-__device__ __forceinline__ float wsum(float x) { return lane_reduce<5, false>(x); }
-__device__ __forceinline__ float wmax(float x) { return lane_reduce<5, true>(x); }
-
-// Two 16x16 output tiles sharing one B column (bf, in registers) over NC
-// 16-wide k chunks, straight-line. The k order inside a chunk is permuted so
-// each lane's four A values are adjacent: MFMA step u of chunk c gives lane
-// group g = l >> 4 the index k = 16c + 4g + u (bf is loaded in the same
-// order), so A comes from LDS as ONE ds_read_b128 per tile per chunk. p0 / p1
-// point at row (l & 15) of each tile plus 4g; pad columns of A and bf are zero.
-template <int NC>
-__device__ __forceinline__ void mfma_pair_b128(f32x4& a0, f32x4& a1, const float* p0, const float* p1,
-                                               const float (&bf)[4 * NC]) {
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const float4 x0 = *reinterpret_cast<const float4*>(p0 + 16 * c);
-    const float4 x1 = *reinterpret_cast<const float4*>(p1 + 16 * c);
-    a0 = mfma16(x0.x, bf[4 * c + 0], a0);
-    a1 = mfma16(x1.x, bf[4 * c + 0], a1);
-    a0 = mfma16(x0.y, bf[4 * c + 1], a0);
-    a1 = mfma16(x1.y, bf[4 * c + 1], a1);
-    a0 = mfma16(x0.z, bf[4 * c + 2], a0);
-    a1 = mfma16(x1.z, bf[4 * c + 2], a1);
-    a0 = mfma16(x0.w, bf[4 * c + 3], a0);
-    a1 = mfma16(x1.w, bf[4 * c + 3], a1);
-  }
-}
-
-// One 16x16 tile (the odd last row tile of a GEMM): the same k order, the
-// chunk's four steps split over two accumulator chains (added at the end) so
-// the 40-cycle dependent MFMA latency stays under the 32-cycle issue interval
-template <int NC>
-__device__ __forceinline__ void mfma_one_b128(f32x4& a0, const float* p0, const float (&bf)[4 * NC]) {
-  f32x4 b0 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const float4 x0 = *reinterpret_cast<const float4*>(p0 + 16 * c);
-    a0 = mfma16(x0.x, bf[4 * c + 0], a0);
-    b0 = mfma16(x0.y, bf[4 * c + 1], b0);
-    a0 = mfma16(x0.z, bf[4 * c + 2], a0);
-    b0 = mfma16(x0.w, bf[4 * c + 3], b0);
-  }
-  a0 += b0;
-}
+// (f32x4, mfma16, the MFMA tile helpers and the shared constants: kge_transr2.h)
+extern template void launch_transr2<SK_P1>(const StepArgs&, const TrArgs&, hipStream_t);
+extern template void launch_transr2<SK_P2>(const StepArgs&, const TrArgs&, hipStream_t);
+extern template void launch_transr2<SK_PINF>(const StepArgs&, const TrArgs&, hipStream_t);
+extern template void launch_transr2<SK_DOT>(const StepArgs&, const TrArgs&, hipStream_t);
+extern template void launch_transr2<SK_PGEN>(const StepArgs&, const TrArgs&, hipStream_t);
 
 template <int SK, int NC>
 __global__ __launch_bounds__(kTrThreads) void transr_kernel(StepArgs A, TrArgs T) {
@@ -778,14 +720,19 @@ template <int SK>
 static void launch_tr(const StepArgs& A, const StepGeom& G, const TrArgs& T, const RelArgs& P, hipStream_t st,
                       hipEvent_t const* ev) {
   if (A.train) launch_rel_rank(P, st);
-  const TrLds L = tr_lds(T.d, T.k, A.Keff);
   const dim3 grid((unsigned)A.B), blk(kTrThreads);
-  const size_t lds = (size_t)L.total_floats * 4;
-  switch (L.NC) {
-    case 4: hipLaunchKernelGGL((transr_kernel<SK, 4>), grid, blk, lds, st, A, T); break;
-    case 8: hipLaunchKernelGGL((transr_kernel<SK, 8>), grid, blk, lds, st, A, T); break;
-    case 13: hipLaunchKernelGGL((transr_kernel<SK, 13>), grid, blk, lds, st, A, T); break;
-    default: hipLaunchKernelGGL((transr_kernel<SK, 16>), grid, blk, lds, st, A, T); break;
+  static const bool v1 = getenv("KGE_TRANSR_V1") != nullptr;   // (A/B timing of the one-per-CU kernel)
+  if (v1) {
+    const TrLds L = tr_lds(T.d, T.k, A.Keff);
+    const size_t lds = (size_t)L.total_floats * 4;
+    switch (L.NC) {
+      case 4: hipLaunchKernelGGL((transr_kernel<SK, 4>), grid, blk, lds, st, A, T); break;
+      case 8: hipLaunchKernelGGL((transr_kernel<SK, 8>), grid, blk, lds, st, A, T); break;
+      case 13: hipLaunchKernelGGL((transr_kernel<SK, 13>), grid, blk, lds, st, A, T); break;
+      default: hipLaunchKernelGGL((transr_kernel<SK, 16>), grid, blk, lds, st, A, T); break;
+    }
+  } else {
+    launch_transr2<SK>(A, T, st);
   }
   if (ev) (void)hipEventRecord(ev[2], st);
   if (A.train) {

@@ -1,0 +1,6 @@
+// transr2_kernel instances for SK_DOT (kge_transr2.h).
+#include "kge_transr2.h"
+
+namespace kge {
+template void launch_transr2<SK_DOT>(const StepArgs&, const TrArgs&, hipStream_t);
+}  // namespace kge

@@ -22,11 +22,16 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "KGE", "_lib", "libkge_hip_trprof.so")
 PHASES = {32: "ids", 33: "gather X", 34: "row stats + GEMM1", 35: "clip", 36: "scores", 37: "loss coefs",
           38: "grads (regs)", 39: "S rows + sums", 40: "GEMM2", 41: "GEMM3", 42: "keys"}
+# transr2_kernel (two per CU, the default; --v1 times transr_kernel)
+PHASES2 = {32: "ids", 33: "gather X", 34: "row stats + GEMM1", 35: "clip + h/t rows", 36: "scores", 37: "loss coefs",
+           38: "passes A-C", 39: "S' rows + GEMM2", 40: "GEMM3", 41: "Q rows + GEMM2 norms", 42: "keys"}
 
 
 def build():
     objs, procs = [], []
-    for src in ("kge_step.hip", "kge_abi.hip", "kge_transr.hip", "kge_rel.hip", "kge_stream.hip", "kge_exchange.hip"):
+    for src in ("kge_step.hip", "kge_abi.hip", "kge_transr.hip", "kge_rel.hip", "kge_stream.hip", "kge_exchange.hip",
+                "kge_transr2_p1.hip", "kge_transr2_p2.hip", "kge_transr2_pinf.hip", "kge_transr2_dot.hip",
+                "kge_transr2_pgen.hip"):
         obj = os.path.join("/tmp", "trprof_" + src.replace(".hip", ".o"))
         cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DKGE_PHASE_PROF", "-DKGE_ONLY_ONE",
                "-c", os.path.join(CSRC, src), "-o", obj]
@@ -39,6 +44,9 @@ def build():
 
 
 def run(args):
+    if args.v1:
+        os.environ["KGE_TRANSR_V1"] = "1"
+    phases = PHASES if args.v1 else PHASES2
     import numpy as np
     import torch
     sys.argv = [sys.argv[0]]
@@ -66,9 +74,9 @@ def run(args):
     step.check_status()
     raw.kge_trprof_read(buf, 64)
     ticks = list(buf)
-    tot = sum(ticks[k] for k in PHASES)
-    print("TransR kernel, B=%d workgroups/step, per-workgroup means over %d steps (10 ns ticks)" % (B, args.steps))
-    for k, label in PHASES.items():
+    tot = sum(ticks[k] for k in phases)
+    print("TransR kernel %s, B=%d workgroups/step, per-workgroup means over %d steps (10 ns ticks)" % ("v1" if args.v1 else "v2", B, args.steps))
+    for k, label in phases.items():
         per = ticks[k] / max(1, args.steps * B)
         print("  %2d %-20s %10.1f ticks/WG  %7.2f us/WG  %5.1f%%" % (k, label, per, per / 100.0,
                                                                     100.0 * ticks[k] / max(1, tot)))
@@ -79,5 +87,6 @@ if __name__ == "__main__":
     ap.add_argument("cmd", choices=["build", "run"])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--v1", action="store_true", help="time the one-workgroup-per-CU kernel")
     a = ap.parse_args()
     build() if a.cmd == "build" else run(a)
