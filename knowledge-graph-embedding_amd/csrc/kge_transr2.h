@@ -89,7 +89,7 @@ __device__ __forceinline__ void mfma_one_b128(f32x4& a0, const float* p0, const 
 // Rows: 0 = h, 1 = t (the positive's slot), 2 + q = negative q.
 struct Tr2Lds {
   int NC, W, LX, NR16;
-  int R, red, ph, pt, rr, pn, xx, xh, xt, sS, sR, sT, sA, dx, dy, ids, misc, total_floats;
+  int R, red, ph, pt, rr, pn, pinv, xx, xh, xt, sS, sR, sT, sA, dx, dy, ids, misc, total_floats;
 };
 __host__ __device__ inline Tr2Lds tr2_lds(int d, int k, int K) {
   Tr2Lds L;
@@ -103,7 +103,7 @@ __host__ __device__ inline Tr2Lds tr2_lds(int d, int k, int K) {
   L.ph = o; o += L.LX;
   L.pt = o; o += L.LX;
   L.rr = o; o += L.LX;
-  int* f[] = {&L.pn, &L.xx, &L.xh, &L.xt, &L.sS, &L.sR, &L.sT, &L.sA, &L.dx, &L.dy};
+  int* f[] = {&L.pn, &L.pinv, &L.xx, &L.xh, &L.xt, &L.sS, &L.sR, &L.sT, &L.sA, &L.dx, &L.dy};
   for (int* p : f) { *p = o; o += L.NR16; }
   L.ids = o; o += (K + 3) & ~3;
   L.misc = o; o += 64;
@@ -146,6 +146,7 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
   float* pts = sm + L.pt;
   float* rrs = sm + L.rr;
   float* pn = sm + L.pn;
+  float* pinv = sm + L.pinv;   // 1 / norm of the rows the clip divides, else 1
   float* xx = sm + L.xx;
   float* xh = sm + L.xh;
   float* xt = sm + L.xt;
@@ -275,7 +276,9 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
     float s = 0.f;
     for (int w = 0; w < kTrWaves; ++w)
       if (w < nct) s += red[w * NR16 + tid];
-    pn[tid] = sqrtf(s);
+    const float n = sqrtf(s);
+    pn[tid] = n;
+    pinv[tid] = (T.clip && !(n < 1.f)) ? 1.f / fmaxf(n, 1e-9f) : 1.f;
   }
   __syncthreads();
 #pragma unroll
@@ -283,12 +286,9 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
     if (rt >= nrt) break;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float n = pn[rt * 16 + g4 + j];
-      if (T.clip && !(n < 1.f)) {
-        const float dv = fmaxf(n, 1e-9f);
+      const float inv = pinv[rt * 16 + g4 + j];   // (1 when the row is not clipped)
 #pragma unroll
-        for (int u = 0; u < 2; ++u) P[u][rt][j] = P[u][rt][j] / dv;
-      }
+      for (int u = 0; u < 2; ++u) P[u][rt][j] *= inv;
     }
   }
   // the positive's projected rows h, t (rows 0, 1: lanes 0-15 of row tile 0) for every wave
@@ -513,8 +513,8 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
       xyp(u, p, own_y, xp, yp);
       grads(xp + rr[u], yp, sA[row], SK == SK_PGEN ? A.p : sR[row], gx, gy);
       const float nx = pn[own_y ? 0 : row], ny = pn[own_y ? row : 1];
-      Gx = (T.clip && !(nx < 1.f)) ? (gx - sdx[row] * xp) / nx : gx;
-      Gy = (T.clip && !(ny < 1.f)) ? (gy - sdy[row] * yp) / ny : gy;
+      Gx = (T.clip && !(nx < 1.f)) ? (gx - sdx[row] * xp) * pinv[own_y ? 0 : row] : gx;
+      Gy = (T.clip && !(ny < 1.f)) ? (gy - sdy[row] * yp) * pinv[own_y ? row : 1] : gy;
       E = own_y ? Gy : Gx;
       Q = own_y ? Gx : Gy;
     };
@@ -608,21 +608,19 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
         if (mt >= nctd) continue;
         const int col = mt * 16 + c16;
         const float* mrow = Mr + (int64_t)(col < d ? col : d - 1) * k;
+        // raw loads into a ring three chunks deep; the bounds mask is applied at
+        // use (a select right after the load would wait for it)
         auto ldb = [&](int c, float (&b)[4]) {
           const int kk = 16 * c + g4;
           if (V4) {
             const float4 m4 = *reinterpret_cast<const float4*>(mrow + (kk < k ? kk : 0));
-            const bool ok = kk < k && col < d;
-            b[0] = ok ? m4.x : 0.f;
-            b[1] = ok ? m4.y : 0.f;
-            b[2] = ok ? m4.z : 0.f;
-            b[3] = ok ? m4.w : 0.f;
+            b[0] = m4.x;
+            b[1] = m4.y;
+            b[2] = m4.z;
+            b[3] = m4.w;
           } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const float v = mrow[kk + q < k ? kk + q : 0];
-              b[q] = (kk + q < k && col < d) ? v : 0.f;
-            }
+            for (int q = 0; q < 4; ++q) b[q] = mrow[kk + q < k ? kk + q : 0];
           }
         };
         f32x4 acc[5];
@@ -634,16 +632,29 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           if (c + 2 < NC) ldb(c + 2, bq[(c + 2) % 3]);
-          const float (&b)[4] = bq[c % 3];
+          float4 xa[5];
 #pragma unroll
-          for (int rt = 0; rt < 5; ++rt) {
-            if (rt >= nrt) break;
-            const float4 x = *reinterpret_cast<const float4*>(X + (rt * 16 + c16) * LX + 16 * c + g4);
-            acc[rt] = mfma16(x.x, b[0], acc[rt]);
-            acc[rt] = mfma16(x.y, b[1], acc[rt]);
-            acc[rt] = mfma16(x.z, b[2], acc[rt]);
-            acc[rt] = mfma16(x.w, b[3], acc[rt]);
-          }
+          for (int rt = 0; rt < 5; ++rt)
+            if (rt < nrt) xa[rt] = *reinterpret_cast<const float4*>(X + (rt * 16 + c16) * LX + 16 * c + g4);
+          // (keep the prefetch two chunks ahead: the occupancy-bound scheduler
+          // would otherwise sink each load to its first use)
+          __builtin_amdgcn_sched_barrier(0);
+          float b[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) b[q] = (16 * c + g4 + q < k && col < d) ? bq[c % 3][q] : 0.f;
+          // k step outer, row tile inner: consecutive MFMAs are independent chains
+#pragma unroll
+          for (int rt = 0; rt < 5; ++rt)
+            if (rt < nrt) acc[rt] = mfma16(xa[rt].x, b[0], acc[rt]);
+#pragma unroll
+          for (int rt = 0; rt < 5; ++rt)
+            if (rt < nrt) acc[rt] = mfma16(xa[rt].y, b[1], acc[rt]);
+#pragma unroll
+          for (int rt = 0; rt < 5; ++rt)
+            if (rt < nrt) acc[rt] = mfma16(xa[rt].z, b[2], acc[rt]);
+#pragma unroll
+          for (int rt = 0; rt < 5; ++rt)
+            if (rt < nrt) acc[rt] = mfma16(xa[rt].w, b[3], acc[rt]);
         }
         if (col >= d) continue;
 #pragma unroll

@@ -28,12 +28,18 @@ PHASES2 = {32: "ids", 33: "gather X", 34: "row stats + GEMM1", 35: "clip + h/t r
 
 
 def build():
+    """The library's objects as build() made them, with kge_transr.hip and the
+    P2 unit of kge_transr2 recompiled with -DKGE_PHASE_PROF."""
+    import __graft_entry__ as g
+    g.build()
+    prof = {"kge_transr.hip", "kge_transr2_p2.hip"}
     objs, procs = [], []
-    for src in ("kge_step.hip", "kge_abi.hip", "kge_transr.hip", "kge_rel.hip", "kge_stream.hip", "kge_exchange.hip",
-                "kge_transr2_p1.hip", "kge_transr2_p2.hip", "kge_transr2_pinf.hip", "kge_transr2_dot.hip",
-                "kge_transr2_pgen.hip"):
+    for src in g.SOURCES:
+        if src not in prof:
+            objs.append(os.path.join(ROOT, "build", "obj", "%s.%s.o" % (src[:-4], g._obj_key(src))))
+            continue
         obj = os.path.join("/tmp", "trprof_" + src.replace(".hip", ".o"))
-        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DKGE_PHASE_PROF", "-DKGE_ONLY_ONE",
+        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DKGE_PHASE_PROF",
                "-c", os.path.join(CSRC, src), "-o", obj]
         procs.append(subprocess.Popen(cmd))
         objs.append(obj)
@@ -54,7 +60,8 @@ def run(args):
     from KGE import _hip, engine
     _hip.load(LIB)
     raw = ctypes.CDLL(LIB)
-    raw.kge_trprof_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    read = raw.kge_trprof_read if args.v1 else raw.kge_trprof2_read   # (each unit counts its own kernel)
+    read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     dev = torch.device("cuda", 0)
     a = argparse.Namespace(batch=args.batch, neg=None, dim=None)
     w = bench.spec("c4-transr", a)
@@ -67,12 +74,12 @@ def run(args):
     for s in range(5):
         step(batches[s], True, opt)
     torch.cuda.synchronize()
-    raw.kge_trprof_read(buf, 64)
+    read(buf, 64)
     for s in range(args.steps):
         step(batches[5 + s], True, opt)
     torch.cuda.synchronize()
     step.check_status()
-    raw.kge_trprof_read(buf, 64)
+    read(buf, 64)
     ticks = list(buf)
     tot = sum(ticks[k] for k in phases)
     print("TransR kernel %s, B=%d workgroups/step, per-workgroup means over %d steps (10 ns ticks)" % ("v1" if args.v1 else "v2", B, args.steps))
