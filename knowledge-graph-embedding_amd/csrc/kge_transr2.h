@@ -86,25 +86,34 @@ __device__ __forceinline__ void mfma_one_b128(f32x4& a0, const float* p0, const 
 // in the wave that owns the column. The entity slices S' are kept in the same
 // register layout. Over X's buffer go first the positive-side slices
 // (re-derived from P) for GEMM2's norm pass, then S' for GEMM2 and GEMM3.
-// Rows: 0 = h, 1 = t (the positive's slot), 2 + q = negative q.
+// Rows of the MFMA tiles: the K negatives (row q = negative q). The positive's
+// h and t rows are not in the tiles (they would cost a fifth 16-row tile for 2
+// rows at K = 64): their projections, back-projections and the rank-2 part of
+// dM are matrix-vector products on the VALU, riding on the M_r columns the
+// MFMA products already hold in registers. Per-row scalars have two more
+// slots: HR = the h row, TR = the t row, which also carries the positive's
+// score (its "slot").
 struct Tr2Lds {
-  int NC, W, LX, NR16;
-  int R, red, ph, pt, rr, pn, pinv, xx, xh, xt, sS, sR, sT, sA, dx, dy, ids, misc, total_floats;
+  int NC, W, LX, NR16, NRR;
+  int R, xht, red, ph, pt, rr, sh, st, qh, qt;
+  int pn, pinv, xx, xh, xt, sS, sR, sT, sA, dx, dy, ids, misc, total_floats;
 };
 __host__ __device__ inline Tr2Lds tr2_lds(int d, int k, int K) {
   Tr2Lds L;
   L.NC = tr_nc(d, k);
   L.W = 16 * L.NC;
   L.LX = L.W + 4;
-  L.NR16 = (K + 2 + 15) & ~15;
+  L.NR16 = (K + 15) & ~15;
+  if (L.NR16 == 0) L.NR16 = 16;
+  L.NRR = L.NR16 + 2;            // + HR, TR
   int o = 0;
-  L.R = o; o += L.NR16 * L.LX;   // X (through GEMM3), then S' rows, then Q rows
-  L.red = o; o += 2 * kTrWaves * L.NR16;   // row reductions: [2][wave role][row]
-  L.ph = o; o += L.LX;
-  L.pt = o; o += L.LX;
-  L.rr = o; o += L.LX;
+  L.R = o; o += L.NR16 * L.LX;   // X (through GEMM1), then the Q rows, then S' rows
+  L.xht = o; o += 2 * L.LX;      // the positive's h, t entity rows
+  L.red = o; o += 2 * kTrWaves * L.NRR;   // row reductions: [2][wave role][row]
+  int* v[] = {&L.ph, &L.pt, &L.rr, &L.sh, &L.st, &L.qh, &L.qt};   // rows of k floats
+  for (int* p : v) { *p = o; o += L.LX; }
   int* f[] = {&L.pn, &L.pinv, &L.xx, &L.xh, &L.xt, &L.sS, &L.sR, &L.sT, &L.sA, &L.dx, &L.dy};
-  for (int* p : f) { *p = o; o += L.NR16; }
+  for (int* p : f) { *p = o; o += L.NRR; }
   L.ids = o; o += (K + 3) & ~3;
   L.misc = o; o += 64;
   L.total_floats = o;
@@ -128,7 +137,7 @@ __device__ __forceinline__ float tr2_col_sum(float v) {
   return a + b;
 }
 
-// NRT: the row-tile count when known at compile time (5: K + 2 > 64, the
+// NRT: the row-tile count when known at compile time (4: 48 < K <= 64, the
 // large-K shapes the kernel is sized for -- straight-line row loops), else 0
 template <int SK, int NC, int NRT>
 __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4))) void transr2_kernel(StepArgs A, TrArgs T) {
@@ -136,17 +145,23 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
   __shared__ float s_w[kTrWaves][4];
   __shared__ int s_last;
   if (ws_refused(A.ctl, A.sig, A.status, A.loss_out)) return;
-  const int d = T.d, k = T.k, K = A.Keff, NR = K + 2;
+  const int d = T.d, k = T.k, K = A.Keff;
   const Tr2Lds L = tr2_lds(d, k, K);
   constexpr int W = 16 * NC;
   const int LX = L.LX, NR16 = NRT ? 16 * NRT : L.NR16, nrt = NRT ? NRT : NR16 >> 4, nct = (k + 15) >> 4;
+  const int NRR = NR16 + 2, HR = NR16, TR = NR16 + 1;
   float* X = sm + L.R;
+  float* XH = sm + L.xht;        // [0] h row, [1] t row
   float* red = sm + L.red;
   float* phs = sm + L.ph;
   float* pts = sm + L.pt;
   float* rrs = sm + L.rr;
+  float* shs = sm + L.sh;        // summed h slices (k)
+  float* sts = sm + L.st;        // summed t slices
+  float* qhs = sm + L.qh;        // the positive's own h slice
+  float* qts = sm + L.qt;        // the positive's own t slice
   float* pn = sm + L.pn;
-  float* pinv = sm + L.pinv;   // 1 / norm of the rows the clip divides, else 1
+  float* pinv = sm + L.pinv;     // 1 / norm of the rows the clip divides, else 1
   float* xx = sm + L.xx;
   float* xh = sm + L.xh;
   float* xt = sm + L.xt;
@@ -162,6 +177,7 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
   KGE_PROF_INIT();
   const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
   const int g4 = 4 * (lane >> 4), c16 = lane & 15;
+  const bool g0 = lane < 16;     // (the positive's values are counted in lane group 0 only)
   const int64_t i = blockIdx.x;
   int err = 0;
   int64_t ph = load_idx(A.pos, i * 3 + 0, A.i64);
@@ -172,20 +188,21 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
   pt = ent_row(A, pt, &err);
   for (int j = tid; j < K; j += kTrThreads) ids[j] = slot_entity(A, i, j, &err);
   __syncthreads();
-  auto row_id = [&](int q) -> int64_t { return q == 0 ? ph : q == 1 ? pt : (int64_t)ids[q - 2]; };
-  // row -> triple kind (row 1 carries the positive; row 0 and pad rows none)
+  // row -> triple kind (TR carries the positive; HR and pad rows none)
   auto rkind = [&](int row) -> int {
-    return row == 1 ? KIND_POS : (row >= 2 && row < NR) ? slot_kind(A.side_mode, row - 2) : -1;
+    return row < K ? slot_kind(A.side_mode, row) : row == TR ? KIND_POS : -1;
   };
 
   KGE_PROF(32);
-  // ---- gather X (pad rows and columns zero), 4 rows' loads in flight per wave
-  for (int row0 = wv; row0 < NR16; row0 += 4 * kTrWaves) {
+  // ---- gather X (the negatives; pad rows and columns zero) and the h, t rows,
+  // 4 rows' loads in flight per wave
+  for (int row0 = wv; row0 < NR16 + 2; row0 += 4 * kTrWaves) {
     float v[4][kTrKV];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int row = row0 + u * kTrWaves;
-      const float* src = row < NR ? A.ent.row(row_id(row)) : nullptr;
+      const float* src = row < K ? A.ent.row(ids[row]) : row == NR16 ? A.ent.row(ph)
+                       : row == NR16 + 1 ? A.ent.row(pt) : nullptr;
 #pragma unroll
       for (int c4 = 0; c4 < kTrKV; ++c4) {
         const int c = lane + KGE_WAVE * c4;
@@ -195,24 +212,26 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int row = row0 + u * kTrWaves;
-      if (row >= NR16) break;
+      if (row >= NR16 + 2) break;
+      float* dst = row < NR16 ? X + row * LX : XH + (row - NR16) * LX;
 #pragma unroll
       for (int c4 = 0; c4 < kTrKV; ++c4) {
         const int c = lane + KGE_WAVE * c4;
-        if (c < W) X[row * LX + c] = v[u][c4];
+        if (c < W) dst[c] = v[u][c4];
       }
     }
   }
   __syncthreads();
   KGE_PROF(33);
-  // row statistics for the rel_proj slice norms: ||x||^2, x.h, x.t
-  for (int row = wv; row < NR; row += kTrWaves) {
+  // row statistics for the rel_proj slice norms: ||x||^2, x.h, x.t (rows K.. NR16: zero)
+  for (int row = wv; row < NRR; row += kTrWaves) {
+    const float* xr = row < NR16 ? X + row * LX : XH + (row - NR16) * LX;
     float a = 0.f, b = 0.f, c2 = 0.f;
     for (int c = lane; c < d; c += KGE_WAVE) {
-      const float x = X[row * LX + c];
+      const float x = xr[c];
       a += x * x;
-      b += X[c] * x;
-      c2 += X[LX + c] * x;
+      b += XH[c] * x;
+      c2 += XH[LX + c] * x;
     }
     a = wsum(a);
     b = wsum(b);
@@ -227,10 +246,13 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
   const bool has0 = w0 < nct, has1 = w0 + 8 < nct;
   const int colu[2] = {16 * w0 + c16, 16 * (w0 + 8) + c16};
   auto has = [&](int u) { return u == 0 ? has0 : has1; };
+  auto live = [&](int u) { return has(u) && colu[u] < k; };
 
-  // ---- GEMM1: P = X M_r, this role's column tiles, every row tile (in pairs)
+  // ---- GEMM1: P = X M_r, this role's column tiles, every row tile (in pairs);
+  // the h / t projections from the same M_r column (VALU, group partials summed)
   const float* Mr = T.proj.row(pr);
   f32x4 P[2][5];
+  float phv[2] = {0.f, 0.f}, ptv[2] = {0.f, 0.f};
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
@@ -254,6 +276,16 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
       if (rt + 1 < 5 && rt + 1 < nrt) mfma_pair_b128<NC>(P[u][rt], P[u][rt + 1 < 5 ? rt + 1 : rt], x0, x0 + 16 * LX, bf);
       else mfma_one_b128<NC>(P[u][rt], x0, bf);
     }
+    float sh_ = 0.f, st_ = 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float4 a = *reinterpret_cast<const float4*>(XH + 16 * c + g4);
+      const float4 b = *reinterpret_cast<const float4*>(XH + LX + 16 * c + g4);
+      sh_ += a.x * bf[4 * c] + a.y * bf[4 * c + 1] + a.z * bf[4 * c + 2] + a.w * bf[4 * c + 3];
+      st_ += b.x * bf[4 * c] + b.y * bf[4 * c + 1] + b.z * bf[4 * c + 2] + b.w * bf[4 * c + 3];
+    }
+    phv[u] = tr2_col_sum(sh_);
+    ptv[u] = tr2_col_sum(st_);
   }
   KGE_PROF(34);
 
@@ -269,13 +301,22 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
       for (int u = 0; u < 2; ++u)
         if (has(u)) x[j] += P[u][rt][j] * P[u][rt][j];
     }
-    tr2_tile_out<false>(x, rt, red + w0 * NR16);
+    tr2_tile_out<false>(x, rt, red + w0 * NRR);
+  }
+  {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (has(u) && g0) { a += phv[u] * phv[u]; b += ptv[u] * ptv[u]; }
+    a = lane_reduce<3, false>(a);
+    b = lane_reduce<3, false>(b);
+    if (lane == 0) { red[w0 * NRR + HR] = a; red[w0 * NRR + TR] = b; }
   }
   __syncthreads();
-  if (tid < NR16) {
+  if (tid < NRR) {
     float s = 0.f;
     for (int w = 0; w < kTrWaves; ++w)
-      if (w < nct) s += red[w * NR16 + tid];
+      if (w < nct) s += red[w * NRR + tid];
     const float n = sqrtf(s);
     pn[tid] = n;
     pinv[tid] = (T.clip && !(n < 1.f)) ? 1.f / fmaxf(n, 1e-9f) : 1.f;
@@ -291,20 +332,24 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
       for (int u = 0; u < 2; ++u) P[u][rt][j] *= inv;
     }
   }
-  // the positive's projected rows h, t (rows 0, 1: lanes 0-15 of row tile 0) for every wave
-  if (lane < 16) {
+  {
+    const float ih = pinv[HR], it = pinv[TR];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) { phv[u] *= ih; ptv[u] *= it; }
+  }
+  // the projected h, t and r (this role's columns) to LDS, re-read after the
+  // products that need the registers
+  if (g0) {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
-      if (has(u)) { phs[colu[u]] = P[u][0][0]; pts[colu[u]] = P[u][0][1]; }
+      if (has(u)) {
+        phs[colu[u]] = phv[u];
+        pts[colu[u]] = ptv[u];
+        rrs[colu[u]] = colu[u] < k ? A.rel.row(pr)[colu[u]] : 0.f;
+      }
   }
-  float rr[2], phv[2], ptv[2];
-  if (lane < 16) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      if (has(u)) rrs[colu[u]] = colu[u] < k ? A.rel.row(pr)[colu[u]] : 0.f;
-  }
+  float rr[2];
   __syncthreads();
-  // (re-read after the products that need the registers: GEMM2 / GEMM3 keep P live)
   auto load_rows = [&]() {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -315,11 +360,17 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
   };
   load_rows();
   // element (row, column tile u): projected x / y rows; scored x = xp + r, y = yp
+  // (p = the row's own projected value; the positive's own row is t)
   auto xyp = [&](int u, float p, bool own_y, float& xp, float& yp) {
     xp = own_y ? phv[u] : p;
     yp = own_y ? p : ptv[u];
   };
-  auto live = [&](int u) { return has(u) && colu[u] < k; };
+  auto score_part = [&](float x, float y, float part) {
+    if (SK == SK_DOT) return part + x * y;
+    const float ma = fabsf(x - y);
+    return SK == SK_P2 ? part + ma * ma : SK == SK_P1 ? part + ma
+         : SK == SK_PGEN ? part + powf(ma, A.p) : fmaxf(part, ma);
+  };
 
   KGE_PROF(35);
   // ---- scores: s(x, y) per row
@@ -337,25 +388,26 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
           if (!live(u)) continue;
           float xp, yp;
           xyp(u, P[u][rt][j], kind != KIND_HC, xp, yp);
-          const float x = xp + rr[u], y = yp;
-          if (SK == SK_DOT) {
-            part += x * y;
-          } else {
-            const float ma = fabsf(x - y);
-            part = SK == SK_P2 ? part + ma * ma : SK == SK_P1 ? part + ma
-                 : SK == SK_PGEN ? part + powf(ma, A.p) : fmaxf(part, ma);
-          }
+          part = score_part(xp + rr[u], yp, part);
         }
       }
       x4[j] = part;
     }
-    tr2_tile_out<SK == SK_PINF>(x4, rt, red + w0 * NR16);
+    tr2_tile_out<SK == SK_PINF>(x4, rt, red + w0 * NRR);
+  }
+  {
+    float part = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (live(u) && g0) part = score_part(phv[u] + rr[u], ptv[u], part);
+    part = lane_reduce<3, SK == SK_PINF>(part);
+    if (lane == 0) red[w0 * NRR + TR] = part;
   }
   __syncthreads();
-  if (tid < NR16) {
+  if (tid < NRR) {
     float R = 0.f;
     for (int w = 0; w < kTrWaves; ++w)
-      if (w < nct) R = SK == SK_PINF ? fmaxf(R, red[w * NR16 + tid]) : R + red[w * NR16 + tid];
+      if (w < nct) R = SK == SK_PINF ? fmaxf(R, red[w * NRR + tid]) : R + red[w * NRR + tid];
     sR[tid] = R;
     if (SK != SK_PINF) {
       float lp;
@@ -386,13 +438,22 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
         }
         x4[j] = tq;
       }
-      tr2_tile_out<false>(x4, rt, red + w0 * NR16);
+      tr2_tile_out<false>(x4, rt, red + w0 * NRR);
+    }
+    {
+      float tq = 0.f;
+      const float M = sR[TR];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (live(u) && g0 && fabsf(phv[u] + rr[u] - ptv[u]) == M) tq += 1.f;
+      tq = lane_reduce<3, false>(tq);
+      if (lane == 0) red[w0 * NRR + TR] = tq;
     }
     __syncthreads();
-    if (tid < NR16) {
+    if (tid < NRR) {
       float t = 0.f;
       for (int w = 0; w < kTrWaves; ++w)
-        if (w < nct) t += red[w * NR16 + tid];
+        if (w < nct) t += red[w * NRR + tid];
       sT[tid] = t;
       float lp;
       sS[tid] = score_value<SK>(sR[tid], A.pw, &lp, A.p);
@@ -403,24 +464,24 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
   KGE_PROF(36);
   // ---- loss and dL/ds per triple (one wave, IEEE transcendentals)
   if (wv == 0) {
-    const float sp = sS[1];
+    const float sp = sS[TR];
     const bool sans = A.loss_kind == KGE_LOSS_SANS;
     float Ms = -INFINITY;
     if (sans)
-      for (int q = lane; q < K; q += KGE_WAVE) Ms = fmaxf(Ms, A.temperature * sS[2 + q]);
+      for (int q = lane; q < K; q += KGE_WAVE) Ms = fmaxf(Ms, A.temperature * sS[q]);
     Ms = wmax(Ms);
     float Z = 0.f;
     if (sans)
-      for (int q = lane; q < K; q += KGE_WAVE) Z += expf(A.temperature * sS[2 + q] - Ms);
+      for (int q = lane; q < K; q += KGE_WAVE) Z += expf(A.temperature * sS[q] - Ms);
     Z = wsum(Z);
     const float invZ = sans ? (Z > 0.f ? 1.f / Z : 0.f) : 1.f;
     float lneg = 0.f, csum = 0.f;
     for (int q = lane; q < K; q += KGE_WAVE) {
-      const float s = sS[2 + q];
+      const float s = sS[q];
       float lp;
-      score_value<SK>(sR[2 + q], A.pw, &lp, A.p);
+      score_value<SK>(sR[q], A.pw, &lp, A.p);
       const float c = neg_coef(A, s, sp, Ms, invZ);
-      sA[2 + q] = score_alpha<SK>(c, sR[2 + q], lp, sT[2 + q], A.pw, A.p);
+      sA[q] = score_alpha<SK>(c, sR[q], lp, sT[q], A.pw, A.p);
       csum += c;
       switch (A.loss_kind) {
         case KGE_LOSS_HINGE: lneg += fmaxf(A.margin + s - sp, 0.f); break;
@@ -445,14 +506,14 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
         default: lossp = ((sp - 1.f) * (sp - 1.f) + lneg) * 0.5f * A.inv_b; cp = (sp - 1.f) * A.inv_b; break;
       }
       float lpp;
-      score_value<SK>(sR[1], A.pw, &lpp, A.p);
-      sA[1] = score_alpha<SK>(cp, sR[1], lpp, sT[1], A.pw, A.p);
+      score_value<SK>(sR[TR], A.pw, &lpp, A.p);
+      sA[TR] = score_alpha<SK>(cp, sR[TR], lpp, sT[TR], A.pw, A.p);
       misc[0] = lossp;
       if (A.pos_score_out) A.pos_score_out[i] = sp;
     }
   }
   if (A.neg_score_out)
-    for (int q = tid; q < K; q += kTrThreads) A.neg_score_out[i * K + q] = sS[2 + q];
+    for (int q = tid; q < K; q += kTrThreads) A.neg_score_out[i * K + q] = sS[q];
   __syncthreads();
 
   KGE_PROF(37);
@@ -493,37 +554,61 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
           }
         }
       }
-      tr2_tile_out<false>(vx, rt, red + w0 * NR16);
-      tr2_tile_out<false>(vy, rt, red + (kTrWaves + w0) * NR16);
+      tr2_tile_out<false>(vx, rt, red + w0 * NRR);
+      tr2_tile_out<false>(vy, rt, red + (kTrWaves + w0) * NRR);
+    }
+    {   // the positive: x = h + r, y = t
+      const float alpha = sA[TR], Mx = SK == SK_PGEN ? A.p : sR[TR];
+      float vx = 0.f, vy = 0.f;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (!live(u) || !g0) continue;
+        float gx, gy;
+        grads(phv[u] + rr[u], ptv[u], alpha, Mx, gx, gy);
+        n_rel += gx * gx;
+        rs[u] += gx;
+        vx += gx * phv[u];
+        vy += gy * ptv[u];
+      }
+      vx = lane_reduce<3, false>(vx);
+      vy = lane_reduce<3, false>(vy);
+      if (lane == 0) { red[w0 * NRR + TR] = vx; red[(kTrWaves + w0) * NRR + TR] = vy; }
     }
     __syncthreads();
-    if (tid < NR16) {
+    if (tid < NRR) {
       float a = 0.f, b = 0.f;
       for (int w = 0; w < kTrWaves; ++w)
-        if (w < nct) { a += red[w * NR16 + tid]; b += red[(kTrWaves + w) * NR16 + tid]; }
+        if (w < nct) { a += red[w * NRR + tid]; b += red[(kTrWaves + w) * NRR + tid]; }
       sdx[tid] = a;
       sdy[tid] = b;
     }
     __syncthreads();
     // the slices back through clip_constraint: Gx (x side), Gy (y side); E = the
-    // row's own entity slice, Q = its positive-side slice
+    // row's own entity slice, Q = its positive-side slice (for the positive's row
+    // TR: E = the t slice, Q = the h slice)
     auto slices = [&](int u, float p, int row, int kind, float& E, float& Q, float& Gx, float& Gy) {
       const bool own_y = kind != KIND_HC;
+      const int xr = own_y ? HR : row, yr = own_y ? row : TR;
       float xp, yp, gx, gy;
       xyp(u, p, own_y, xp, yp);
       grads(xp + rr[u], yp, sA[row], SK == SK_PGEN ? A.p : sR[row], gx, gy);
-      const float nx = pn[own_y ? 0 : row], ny = pn[own_y ? row : 1];
-      Gx = (T.clip && !(nx < 1.f)) ? (gx - sdx[row] * xp) * pinv[own_y ? 0 : row] : gx;
-      Gy = (T.clip && !(ny < 1.f)) ? (gy - sdy[row] * yp) * pinv[own_y ? row : 1] : gy;
+      Gx = (T.clip && !(pn[xr] < 1.f)) ? (gx - sdx[row] * xp) * pinv[xr] : gx;
+      Gy = (T.clip && !(pn[yr] < 1.f)) ? (gy - sdy[row] * yp) * pinv[yr] : gy;
       E = own_y ? Gy : Gx;
       Q = own_y ? Gx : Gy;
     };
     // ---- pass B: the slices; S' (this role's columns, accumulator layout) = the
-    // entity slices, rows 0 / 1 the summed h / t slices; the rel_proj slice norms
-    // ||x_x (x) Gx + x_y (x) Gy||^2 summed element by element (per-row scalars
-    // times per-element squares: no row reduction)
+    // negatives' entity slices; the summed h / t slices per column; the rel_proj
+    // slice norms ||x_x (x) Gx + x_y (x) Gy||^2 summed element by element
+    // (per-row scalars times per-element squares: no row reduction)
     f32x4 SP[2][5];
     float sh[2] = {0.f, 0.f}, st[2] = {0.f, 0.f};
+    auto nproj = [&](int row, int kind, float Gx, float Gy) {
+      const bool own_y = kind != KIND_HC;
+      const float hx = xx[own_y ? HR : row], tx = xx[own_y ? row : TR];
+      const float htx = kind == KIND_TC ? xh[row] : kind == KIND_HC ? xt[row] : xh[TR];
+      return hx * (Gx * Gx) + tx * (Gy * Gy) + 2.f * htx * (Gx * Gy);
+    };
 #pragma unroll
     for (int rt = 0; rt < 5; ++rt) {
 #pragma unroll
@@ -534,20 +619,28 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
         const int row = rt * 16 + g4 + j;
         const int kind = rkind(row);
         if (kind < 0) continue;
-        const bool own_y = kind != KIND_HC;
-        const float hx = xx[own_y ? 0 : row], tx = xx[own_y ? row : 1];
-        const float htx = kind == KIND_POS ? xh[1] : (kind == KIND_TC ? xh[row] : xt[row]);
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           if (!live(u)) continue;
           float E, Q, Gx, Gy;
           slices(u, P[u][rt][j], row, kind, E, Q, Gx, Gy);
-          n_proj += hx * (Gx * Gx) + tx * (Gy * Gy) + 2.f * htx * (Gx * Gy);
-          if (own_y) sh[u] += Q; else st[u] += Q;
-          if (kind == KIND_POS) st[u] += E;
+          n_proj += nproj(row, kind, Gx, Gy);
+          if (kind != KIND_HC) sh[u] += Q; else st[u] += Q;
           SP[u][rt][j] = E;
         }
       }
+    }
+    float qh[2] = {0.f, 0.f}, qt[2] = {0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!live(u) || !g0) continue;
+      float E, Q, Gx, Gy;
+      slices(u, ptv[u], TR, KIND_POS, E, Q, Gx, Gy);
+      n_proj += nproj(TR, KIND_POS, Gx, Gy);
+      qh[u] = Q;
+      qt[u] = E;
+      sh[u] += Q;
+      st[u] += E;
     }
     float* gp = A.gpos + i * 3 * (int64_t)A.gcols;
 #pragma unroll
@@ -555,19 +648,25 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
       rs[u] = tr2_col_sum(rs[u]);
       sh[u] = tr2_col_sum(sh[u]);
       st[u] = tr2_col_sum(st[u]);
-      if (lane < 16 && live(u)) {
-        gp[A.gcols + colu[u]] = rs[u];
-        SP[u][0][0] = sh[u];   // (rows 0 / 1: lanes 0-15 of row tile 0)
-        SP[u][0][1] = st[u];
+      if (g0 && has(u)) {
+        const bool lv = colu[u] < k;
+        if (lv) gp[A.gcols + colu[u]] = rs[u];
+        shs[colu[u]] = lv ? sh[u] : 0.f;
+        sts[colu[u]] = lv ? st[u] : 0.f;
+        qhs[colu[u]] = lv ? qh[u] : 0.f;
+        qts[colu[u]] = lv ? qt[u] : 0.f;
       }
+    }
+    if (tid < W - 16 * nct) {   // (the row vectors' columns past P's tiles)
+      const int c = 16 * nct + tid;
+      shs[c] = sts[c] = qhs[c] = qts[c] = 0.f;
     }
 
     KGE_PROF(38);
     __syncthreads();   // (X is dead since GEMM1) the positive-side slices over it
     KGE_PROF(39);
     load_rows();
-    // ---- Q rows: [0] the positive's t slice, [1] its h slice, [2 + q] negative q's
-    // positive-side slice -> GEMM2's norms
+    // ---- Q rows: negative q's positive-side slice -> GEMM2's norms
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (!has(u)) continue;
@@ -577,14 +676,12 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int row = rt * 16 + g4 + j;
+          const int kind = rkind(row);
           float val = 0.f;
-          // row 0 takes the positive's t slice: row 1's element, this lane's register j = 1
-          const bool r0 = row == 0;
-          const int srow = r0 ? 1 : row, kind = rkind(srow);
           if (colu[u] < k && kind >= 0) {
             float E, Q, Gx, Gy;
-            slices(u, (rt == 0 && j == 0) ? (r0 ? P[u][0][1] : P[u][0][0]) : P[u][rt][j], srow, kind, E, Q, Gx, Gy);
-            val = r0 ? E : Q;
+            slices(u, P[u][rt][j], row, kind, E, Q, Gx, Gy);
+            val = Q;
           }
           X[row * LX + colu[u]] = val;
         }
@@ -597,10 +694,14 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
     __syncthreads();
     // ---- GEMM2: Y = S M_r^T over the staged rows; job = one 16-column tile of
     // Y (d) over every row tile, M_r^T's column streamed chunk by chunk (two
-    // chunks ahead). NORMS = false: rows 0 / 1 -> the positive's h / t gradient
-    // rows, rows 2 + q -> gneg[code] (+ norms); NORMS = true: ||.||^2 only.
+    // chunks ahead). Two k-vectors ride on the same column (VALU): NORMS = false:
+    // S' rows -> gneg[code] (+ norms), the summed h / t slices -> the positive's
+    // gradient rows; NORMS = true: ||.||^2 of the Q rows and of the positive's
+    // own h / t slices.
     auto gemm2 = [&](auto norms, auto vec4) {
       constexpr bool NORMS = decltype(norms)::value, V4 = decltype(vec4)::value;
+      const float* va = NORMS ? qhs : shs;
+      const float* vb = NORMS ? qts : sts;
       const int nctd = (d + 15) / 16;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -626,6 +727,7 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
         f32x4 acc[5];
 #pragma unroll
         for (int rt = 0; rt < 5; ++rt) acc[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float ya = 0.f, yb = 0.f;
         float bq[3][4];
         ldb(0, bq[0]);
         if (NC > 1) ldb(1, bq[1]);
@@ -636,6 +738,8 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
           for (int rt = 0; rt < 5; ++rt)
             if (rt < nrt) xa[rt] = *reinterpret_cast<const float4*>(X + (rt * 16 + c16) * LX + 16 * c + g4);
+          const float4 a4 = *reinterpret_cast<const float4*>(va + 16 * c + g4);
+          const float4 b4 = *reinterpret_cast<const float4*>(vb + 16 * c + g4);
           // (keep the prefetch two chunks ahead: the occupancy-bound scheduler
           // would otherwise sink each load to its first use)
           __builtin_amdgcn_sched_barrier(0);
@@ -655,8 +759,20 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
           for (int rt = 0; rt < 5; ++rt)
             if (rt < nrt) acc[rt] = mfma16(xa[rt].w, b[3], acc[rt]);
+          ya += a4.x * b[0] + a4.y * b[1] + a4.z * b[2] + a4.w * b[3];
+          yb += b4.x * b[0] + b4.y * b[1] + b4.z * b[2] + b4.w * b[3];
         }
+        ya = tr2_col_sum(ya);
+        yb = tr2_col_sum(yb);
         if (col >= d) continue;
+        if (g0) {
+          if (NORMS) {
+            n_ent += ya * ya + yb * yb;
+          } else {
+            gp[col] = ya;
+            gp[2 * A.gcols + col] = yb;
+          }
+        }
 #pragma unroll
         for (int rt = 0; rt < 5; ++rt) {
           if (rt >= nrt) break;
@@ -664,15 +780,9 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
           for (int q = 0; q < 4; ++q) {
             const int row = rt * 16 + g4 + q;
             const float v = acc[rt][q];
-            if (NORMS) {
-              if (row < NR) n_ent += v * v;
-            } else if (row == 0) {
-              gp[col] = v;
-            } else if (row == 1) {
-              gp[2 * A.gcols + col] = v;
-            } else if (row < NR) {
+            if (row < K) {
               n_ent += v * v;
-              A.gneg[(int64_t)(((uint32_t)i << A.kshift) | (uint32_t)(row - 2)) * d + col] = v;
+              if (!NORMS) A.gneg[(int64_t)(((uint32_t)i << A.kshift) | (uint32_t)row) * d + col] = v;
             }
           }
         }
@@ -694,16 +804,14 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
         for (int j = 0; j < 4; ++j) X[(rt * 16 + g4 + j) * LX + colu[u]] = SP[u][rt][j];
       }
     }
-    {
-      const int c0 = 16 * nct, wpad = W - c0;
-      for (int e = tid; e < NR16 * wpad; e += kTrThreads) X[(e / wpad) * LX + c0 + e % wpad] = 0.f;
-    }
     __syncthreads();
 
     if (mv4) gemm2(std::false_type{}, std::true_type{});
     else gemm2(std::false_type{}, std::false_type{});
-    // ---- GEMM3: dM_i = X^T S' (S' rows in LDS, X re-read from the table: L2);
-    // job = 16-row tile of dM (its A column in registers) x a pair of column tiles
+    // ---- GEMM3: dM_i = X^T S' + x_h^T (sum of h slices) + x_t^T (sum of t slices)
+    // (S' rows in LDS, X re-read from the table: L2; the rank-2 part in the
+    // epilogue); job = 16-row tile of dM (its A column in registers) x a pair of
+    // column tiles
     {
       auto gemm3 = [&](auto n3c) {
         constexpr int N3 = decltype(n3c)::value;
@@ -722,8 +830,8 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
 #pragma unroll
             for (int ks = 0; ks < kTrKS3; ++ks) {
               const int kk = ks * 4 + (lane >> 4);
-              const float v = A.ent.row(row_id(kk < NR ? kk : 0))[cic];
-              af[ks] = (kk < NR && ci < d) ? v : 0.f;
+              const float v = A.ent.row(ids[kk < K ? kk : 0])[cic];
+              af[ks] = (kk < K && ci < d) ? v : 0.f;
             }
           }
           const int ct1 = ct + 1 < nct ? ct + 1 : ct;
@@ -760,15 +868,17 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
             if (h == 1 && !pair) break;
             const int col = (h ? ct1 : ct) * 16 + c16;
             if (col >= k) continue;
+            const float sgh = shs[col], sgt = sts[col];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               const int row = rt * 16 + g4 + q;
-              if (row < d) dm[(int64_t)row * k + col] = (h ? a1 : a0)[q];
+              if (row < d) dm[(int64_t)row * k + col] = (h ? a1 : a0)[q] + XH[row] * sgh + XH[LX + row] * sgt;
             }
           }
         }
       };
       if (nrt == kTrKS3 / 4) gemm3(std::integral_constant<int, kTrKS3 / 4>{});
+      else if (nrt == 4) gemm3(std::integral_constant<int, 4>{});
       else gemm3(std::integral_constant<int, 0>{});
     }
     KGE_PROF(41);
@@ -842,7 +952,7 @@ void launch_transr2(const StepArgs& A, const TrArgs& T, hipStream_t st) {
       default: hipLaunchKernelGGL((transr2_kernel<SK, 16, R>), grid, blk, lds, st, A, T); break;
     }
   };
-  if (L.NR16 == 80) go(std::integral_constant<int, 5>{});
+  if (L.NR16 == 64) go(std::integral_constant<int, 4>{});
   else go(std::integral_constant<int, 0>{});
 }
 
