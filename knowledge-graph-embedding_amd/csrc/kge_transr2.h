@@ -194,13 +194,14 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
   };
 
   KGE_PROF(32);
-  // ---- gather X (the negatives; pad rows and columns zero) and the h, t rows,
-  // 4 rows' loads in flight per wave
-  for (int row0 = wv; row0 < NR16 + 2; row0 += 4 * kTrWaves) {
-    float v[4][kTrKV];
+  // ---- gather X (the negatives; pad rows and columns zero) and the h, t rows:
+  // a wave's rows (row = wave + 8 u) all in flight at once
+  {
+    constexpr int GU = ((NRT ? 16 * NRT : 80) + 2 + kTrWaves - 1) / kTrWaves;   // rows per wave
+    float v[GU][kTrKV];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int row = row0 + u * kTrWaves;
+    for (int u = 0; u < GU; ++u) {
+      const int row = wv + u * kTrWaves;
       const float* src = row < K ? A.ent.row(ids[row]) : row == NR16 ? A.ent.row(ph)
                        : row == NR16 + 1 ? A.ent.row(pt) : nullptr;
 #pragma unroll
@@ -210,8 +211,8 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int row = row0 + u * kTrWaves;
+    for (int u = 0; u < GU; ++u) {
+      const int row = wv + u * kTrWaves;
       if (row >= NR16 + 2) break;
       float* dst = row < NR16 ? X + row * LX : XH + (row - NR16) * LX;
 #pragma unroll
