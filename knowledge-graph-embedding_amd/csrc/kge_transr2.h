@@ -137,8 +137,8 @@ __device__ __forceinline__ float tr2_col_sum(float v) {
   return a + b;
 }
 
-// NRT: the row-tile count when known at compile time (4: 48 < K <= 64, the
-// large-K shapes the kernel is sized for -- straight-line row loops), else 0
+// NRT: the row-tile count, 1..5 (straight-line row loops; a runtime count
+// made the row loops' guards real branches, and the products spilled)
 template <int SK, int NC, int NRT>
 __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4))) void transr2_kernel(StepArgs A, TrArgs T) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
   const int d = T.d, k = T.k, K = A.Keff;
   const Tr2Lds L = tr2_lds(d, k, K);
   constexpr int W = 16 * NC;
-  const int LX = L.LX, NR16 = NRT ? 16 * NRT : L.NR16, nrt = NRT ? NRT : NR16 >> 4, nct = (k + 15) >> 4;
+  const int LX = L.LX, NR16 = 16 * NRT, nrt = NRT, nct = (k + 15) >> 4;
   const int NRR = NR16 + 2, HR = NR16, TR = NR16 + 1;
   float* X = sm + L.R;
   float* XH = sm + L.xht;        // [0] h row, [1] t row
@@ -197,7 +197,7 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
   // ---- gather X (the negatives; pad rows and columns zero) and the h, t rows:
   // a wave's rows (row = wave + 8 u) all in flight at once
   {
-    constexpr int GU = ((NRT ? 16 * NRT : 80) + 2 + kTrWaves - 1) / kTrWaves;   // rows per wave
+    constexpr int GU = (16 * NRT + 2 + kTrWaves - 1) / kTrWaves;   // rows per wave
     float v[GU][kTrKV];
 #pragma unroll
     for (int u = 0; u < GU; ++u) {
@@ -878,8 +878,7 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
           }
         }
       };
-      if (nrt == kTrKS3 / 4) gemm3(std::integral_constant<int, kTrKS3 / 4>{});
-      else if (nrt == 4) gemm3(std::integral_constant<int, 4>{});
+      if (NRT) gemm3(std::integral_constant<int, NRT>{});   // (straight-line chunk loop)
       else gemm3(std::integral_constant<int, 0>{});
     }
     KGE_PROF(41);
@@ -953,8 +952,13 @@ void launch_transr2(const StepArgs& A, const TrArgs& T, hipStream_t st) {
       default: hipLaunchKernelGGL((transr2_kernel<SK, 16, R>), grid, blk, lds, st, A, T); break;
     }
   };
-  if (L.NR16 == 64) go(std::integral_constant<int, 4>{});
-  else go(std::integral_constant<int, 0>{});
+  switch (L.NR16 >> 4) {   // (K <= kTrMaxSlots - 1: at most five row tiles)
+    case 1: go(std::integral_constant<int, 1>{}); break;
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 3: go(std::integral_constant<int, 3>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    default: go(std::integral_constant<int, 5>{}); break;
+  }
 }
 
 }  // namespace kge
