@@ -913,7 +913,8 @@ class ShardedStep:
         # 2. every rank's positives: rows (h, t of positive v at pos_base + 2v, + 1) and triples
         P = ext[b["pos_base"]:b["pos_base"] + 2 * G * Bn]
         mine = P[2 * g * Bn:2 * (g + 1) * Bn]
-        mine.copy_(ext.index_select(0, lpos[:, 0::2].reshape(-1).to(torch.int64)))   # (a view of ext: no out=)
+        # (gathered straight into P: the source rows [0, pos_base) and P do not overlap)
+        torch.index_select(ext[:b["pos_base"]], 0, lpos[:, 0::2].reshape(-1).to(torch.int64), out=mine)
         gtrip = o["gtrip"]
         if G > 1:   # (one rank: P is `mine`, the virtual batch is the batch)
             ex.all_gather(P, mine)
