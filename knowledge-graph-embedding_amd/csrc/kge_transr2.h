@@ -240,10 +240,13 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
     if (lane == 0) { xx[row] = a; xh[row] = b; xt[row] = c2; }
   }
 
-  // wave role: P column tiles w0 and w0 + 8. Workgroups adjacent on an XCD
-  // (blockIdx + 8) shift the roles by two waves, so the roles holding a
-  // second tile fall on different SIMDs in the two resident workgroups.
-  const int w0 = (wv - 2 * ((int)(blockIdx.x >> 3) & 1)) & (kTrWaves - 1);
+  // wave role: P column tiles w0 and w0 + 8. The two workgroups resident on a
+  // CU shift their roles by two waves against each other, so the roles holding
+  // a second tile fall on different SIMDs. On an XCD (blockIdx mod 8) the
+  // local index j = blockIdx / 8 goes round-robin over 32 CUs (pair j, j + 32)
+  // or fills a CU first (pair 2c, 2c + 1): bit 0 of j ^ (j >> 5) differs in both.
+  const int jx = (int)(blockIdx.x >> 3);
+  const int w0 = (wv - 2 * ((jx ^ (jx >> 5)) & 1)) & (kTrWaves - 1);
   const bool has0 = w0 < nct, has1 = w0 + 8 < nct;
   const int colu[2] = {16 * w0 + c16, 16 * (w0 + 8) + c16};
   auto has = [&](int u) { return u == 0 ? has0 : has1; };
