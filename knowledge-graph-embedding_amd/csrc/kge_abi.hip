@@ -955,22 +955,18 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   if (P.proj && d->constraint && !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT)) {
     // _constraint_loss assigns: TransH normalises rel_hyper (TransH.py:202);
     // TransD clips ent_emb and rel_emb (TransD.py:238-240)
-    const kge_table* tabs[2] = {P.td ? &d->ent : &d->rel_aux, &d->rel};
-    for (int v = 0; v < (P.td ? 2 : 1); ++v) {
-      const int64_t blocks = std::min<int64_t>(ceil_div(tabs[v]->rows, kWaves), 4096);
-      hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, tabs[v]->data,
-                         tabs[v]->rows, (int32_t)tabs[v]->cols, tabs[v]->ld, P.td ? 1 : 0, 1.0f, A.ctl, A.sig,
-                         A.status);
-    }
+    const kge_table& t0 = P.td ? d->ent : d->rel_aux;
+    const int64_t blocks = std::min<int64_t>(ceil_div(t0.rows + (P.td ? d->rel.rows : 0), kWaves), 4096);
+    hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, t0.data, t0.rows,
+                       (int32_t)t0.cols, t0.ld, P.td ? 1 : 0, 1.0f, A.ctl, A.sig, A.status,
+                       P.td ? d->rel.data : (float*)nullptr, d->rel.rows, (int32_t)d->rel.cols, d->rel.ld);
   }
   if (P.transr && d->constraint && !(d->flags & KGE_FLAG_NO_TABLE_CONSTRAINT)) {
     // _constraint_loss assigns (TransR.py:207-209): clip every entity and relation row to norm <= 1
-    const kge_table* tabs[2] = {&d->ent, &d->rel};
-    for (int v = 0; v < 2; ++v) {
-      const int64_t blocks = std::min<int64_t>(ceil_div(tabs[v]->rows, kWaves), 4096);
-      hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, tabs[v]->data,
-                         tabs[v]->rows, (int32_t)tabs[v]->cols, tabs[v]->ld, 1, 1.0f, A.ctl, A.sig, A.status);
-    }
+    const int64_t blocks = std::min<int64_t>(ceil_div(d->ent.rows + d->rel.rows, kWaves), 4096);
+    hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, d->ent.data, d->ent.rows,
+                       (int32_t)d->ent.cols, d->ent.ld, 1, 1.0f, A.ctl, A.sig, A.status, d->rel.data, d->rel.rows,
+                       (int32_t)d->rel.cols, d->rel.ld);
   }
   // _constraint_loss assigns before scoring (BaseModel.py:319): fused into
   // the score / update kernels on the SGD path (A.fuse_norm), else K0
@@ -979,7 +975,8 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
   if (renorm && !(A.fuse_norm && d->batch > 0)) {
     const int64_t blocks = std::min<int64_t>(ceil_div(d->ent.rows, kWaves), 4096);
     hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, st, d->ent.data,
-                       d->ent.rows, (int32_t)d->ent.cols, d->ent.ld, 0, 1.0f, A.ctl, A.sig, A.status);
+                       d->ent.rows, (int32_t)d->ent.cols, d->ent.ld, 0, 1.0f, A.ctl, A.sig, A.status,
+                       (float*)nullptr, (int64_t)0, 0, (int64_t)0);
   }
   if (d->batch == 0) {
     (void)hipMemsetAsync(d->loss_out, 0, sizeof(float), st);
@@ -1098,7 +1095,7 @@ kge_status kge_constrain_rows(kge_table t, int32_t kind, float value, void* stre
   const int64_t blocks = std::min<int64_t>(ceil_div(t.rows, kWaves), 4096);
   hipLaunchKernelGGL(constrain_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, t.data,
                      t.rows, (int32_t)t.cols, t.ld, kind, value, (StepCtl*)nullptr, 0u,
-                     (int32_t*)nullptr);
+                     (int32_t*)nullptr, (float*)nullptr, (int64_t)0, 0, (int64_t)0);
   return hip_check("kge_constrain_rows");
 }
 

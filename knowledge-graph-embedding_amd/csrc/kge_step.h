@@ -436,7 +436,8 @@ void launch_stream_gather(const void* tri, bool i64, int64_t n, int64_t start, i
                           const int32_t* phi, int64_t e0, void* out, hipStream_t st);
 
 __global__ void constrain_rows_kernel(float* t, int64_t rows, int32_t cols, int64_t ld, int kind,
-                                      float value, StepCtl* ctl, uint32_t sig, int32_t* status);
+                                      float value, StepCtl* ctl, uint32_t sig, int32_t* status,
+                                      float* t2, int64_t rows2, int32_t cols2, int64_t ld2);
 
 // Byte offsets of the score kernel's dynamic LDS carve (shared by host and
 // device so the launch size always matches the kernel's view).

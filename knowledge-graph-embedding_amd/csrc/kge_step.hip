@@ -35,12 +35,11 @@ namespace kge {
 // ------------------------------------------------------------ K0 constrain
 // kind 0: normalized_embeddings(p=2) -> X / pow(sum X^2, 1/2) * value
 // kind 1: clip_constraint(p=2)       -> rows with norm >= value rescaled
-// Each wave owns 4 rows and issues all their loads before reducing.
-__global__ __launch_bounds__(256) void constrain_rows_kernel(float* __restrict__ t, int64_t rows,
-                                                              int32_t cols, int64_t ld, int kind,
-                                                              float value, StepCtl* ctl, uint32_t sig,
-                                                              int32_t* status) {
-  if (ctl && ws_refused(ctl, sig, status, nullptr)) return;   // launched by a step: guarded
+// Each wave owns 4 rows and issues all their loads before reducing. A second
+// table (t2, may be null) is constrained in the same launch (TransR / TransD
+// clip ent_emb and rel_emb: one launch, not two).
+__device__ __forceinline__ void constrain_table(float* __restrict__ t, int64_t rows, int32_t cols, int64_t ld,
+                                                int kind, float value) {
   constexpr int RPW = 4;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x / KGE_WAVE);
   const bool v4 = (cols % 4 == 0) && (ld % 4 == 0) && (((uintptr_t)t & 15) == 0) && cols <= 4 * KGE_WAVE;
@@ -93,6 +92,16 @@ __global__ __launch_bounds__(256) void constrain_rows_kernel(float* __restrict__
       }
     }
   }
+}
+
+__global__ __launch_bounds__(256) void constrain_rows_kernel(float* __restrict__ t, int64_t rows,
+                                                              int32_t cols, int64_t ld, int kind,
+                                                              float value, StepCtl* ctl, uint32_t sig,
+                                                              int32_t* status, float* __restrict__ t2,
+                                                              int64_t rows2, int32_t cols2, int64_t ld2) {
+  if (ctl && ws_refused(ctl, sig, status, nullptr)) return;   // launched by a step: guarded
+  constrain_table(t, rows, cols, ld, kind, value);
+  if (t2) constrain_table(t2, rows2, cols2, ld2, kind, value);
 }
 
 // ------------------------------------------------------------ apply
