@@ -287,10 +287,13 @@ def test_transr(hiplib, si, li):
 
 
 @pytest.mark.parametrize("d,k,B,K,side,constraint", [(200, 200, 6, 64, "h+t", True), (32, 48, 17, 3, "t", True),
-                                                      (40, 16, 9, 5, "h", False), (17, 33, 5, 70, "h+t", True)])
+                                                      (40, 16, 9, 5, "h", False), (17, 33, 5, 70, "h+t", True),
+                                                      (100, 120, 5, 20, "h+t", True), (240, 256, 4, 40, "t", True)])
 def test_transr_shapes(hiplib, d, k, B, K, side, constraint):
     """C4's TransR shape (d = k = 200, K = 64) at reduced batch; odd sizes;
-    the constraint off (no clip, no table assigns)."""
+    the constraint off (no clip, no table assigns). Together the cases reach
+    every row-tile count (1-5: K + 0..15 rounded to 16) and column-chunk count
+    (4, 8, 13, 16) the two-per-CU kernel is instantiated for."""
     from KGE import loss, score
     ref, got, l_, ps, ns, _, _ = run_case(hiplib, "TransR", d, B, K, side, score.LpDistancePow(2),
                                           loss.PairwiseHingeLoss(1.0), k=k, constraint=constraint, E=90, R=4)
