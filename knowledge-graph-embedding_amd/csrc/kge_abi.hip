@@ -566,20 +566,7 @@ __global__ __launch_bounds__(256) void phase_gate_kernel(StepCtl* ctl, uint32_t 
                                                          float* zero, int64_t n) {
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (int64_t)gridDim.x * blockDim.x)
     zero[q] = 0.f;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    // vector (atomic) loads, and the reset only after p is known: plain
-    // loads of these uniform words become scalar loads, which the reset's
-    // vector store may overtake (it would read its own 0)
-    const uint32_t s = __hip_atomic_load(&ctl->plan_sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t p = __hip_atomic_load(&ctl->score_pending, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (p != 0u) __hip_atomic_store(&ctl->score_pending, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (s != sig || p != sig) {
-      // (s is another plan's: its kernels refuse the workspace anyway; 0: the
-      // update pass would claim a fresh workspace and run on empty lists)
-      if (s == 0u || s == sig) __hip_atomic_store(&ctl->plan_sig, kPoisonedSig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      set_status(status, KGE_EWORKSPACE);
-    }
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) phase_gate_check(ctl, sig, status);   // (kge_owner.h)
 }
 
 static void launch_phase_gate(StepCtl* ctl, uint32_t sig, int32_t* status, float* zero, int64_t n, hipStream_t st) {
@@ -819,7 +806,7 @@ kge_status kge_step(const kge_step_desc* d, void* stream) {
     if (d->batch > 0) {
       // the phase gate; the merge's relation gradients start from zero
       // (rel_seg writes every row's every column itself)
-      if (upd && !(P.omerge && P.seg)) {   // (the segmented merge update gates itself)
+      if (upd && !P.own && !(P.omerge && P.seg)) {   // (owner_coef_kernel and the segmented merge update gate themselves)
         const bool zero = P.omerge && !(A.rel_seg && A.rel_gcols == A.rel.cols);
         launch_phase_gate(A.ctl, A.sig, A.status, zero ? d->grad_out[1] : nullptr,
                           zero ? A.rel.rows * (int64_t)A.rel_gcols : 0, st);

@@ -244,11 +244,34 @@ __global__ __launch_bounds__(kMergeWaves * KGE_WAVE) void owner_merge_kernel(Ste
   }
 }
 
+// The split step's phase gate, one thread (phase_gate_kernel, kge_abi.hip):
+// the score pass's token read and cleared; a missing / foreign one poisons
+// the workspace (every guarded kernel after it refuses) and sets the status.
+// Vector (atomic) loads, and the reset only after p is known: plain loads of
+// these uniform words become scalar loads, which the reset's vector store
+// may overtake (it would read its own 0).
+__device__ __forceinline__ void phase_gate_check(StepCtl* ctl, uint32_t sig, int32_t* status) {
+  const uint32_t s = __hip_atomic_load(&ctl->plan_sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t p = __hip_atomic_load(&ctl->score_pending, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (p != 0u) __hip_atomic_store(&ctl->score_pending, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (s != sig || p != sig) {
+    // (s is another plan's: its kernels refuse the workspace anyway; 0: the
+    // update pass would claim a fresh workspace and run on empty lists)
+    if (s == 0u || s == sig) __hip_atomic_store(&ctl->plan_sig, kPoisonedSig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    set_status(status, KGE_EWORKSPACE);
+  }
+}
+
 // Each owned negative's coefficient from its (R, ties) and its positive's
 // global softmax state: the score kernel's finalise pass (neg_coef,
-// score_alpha) with (Ms, 1/Z, s_pos) from the merge.
+// score_alpha) with (Ms, 1/Z, s_pos) from the merge. The owner update pass's
+// first launch, so it carries the phase gate (thread 0 of block 0). The
+// other threads may still compute coefficients for a refused pass: they
+// write only workspace scratch, and the update kernel after this launch
+// refuses the poisoned workspace.
 template <int SK>
 __global__ __launch_bounds__(256) void owner_coef_kernel(StepArgs A) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) phase_gate_check(A.ctl, A.sig, A.status);
   if (ws_refused(A.ctl, A.sig, A.status, nullptr)) return;
   if (A.abort_flag && *A.abort_flag != 0.f) return;
   const uint32_t n = min(A.ctl->own_len, A.own_cap);

@@ -1281,6 +1281,45 @@ def test_compact_hot_relation(hiplib, model_name):
     check(ref, got, l_, ps, ns)
 
 
+def test_owner_update_phase_needs_its_score_pass(hiplib):
+    """The owner update pass gates itself (owner_coef_kernel carries the
+    split step's phase gate): replayed after a full owner step, with no owner
+    score pass before it, it is refused on the device (KGE_EWORKSPACE) and
+    writes no table row."""
+    import torch.distributed as dist
+    from KGE import _hip, loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    from KGE.sharded import ShardedStep
+    dev = _dev()
+    _init_world1(dist, dev)
+    try:
+        E, R, d, B, K = 50000, 5, 24, 64, 8
+        rng = np.random.default_rng(71)
+        W = _weights("TransE", E, R, d, rng)
+        m = _make("TransE", d, K, "h+t", score.LpDistance(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
+                  E, R, UniformStrategy(np.arange(E), seed=5), constraint=False)
+        m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
+        st = ShardedStep(m, mode="owner", local_fast=False)
+        opt = optimizers.SGD(0.05)
+        pos = np.stack([rng.integers(0, E, B), rng.integers(0, R, B), rng.integers(0, E, B)], 1).astype(np.int64)
+        bt = torch.tensor(pos, device=dev)
+        st(bt, True, opt)
+        torch.cuda.synchronize()
+        st.check_status()
+        shard = st.shard.clone()
+        o = st._own
+        fo = o["fo"]
+        fo.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER | _hip.FLAG_PHASE_UPDATE
+        fo.abort = None
+        st.status.zero_()
+        fo(bt, True, opt)
+        torch.cuda.synchronize()
+        assert int(st.status.item()) == _hip.KGE_EWORKSPACE
+        assert torch.equal(st.shard, shard)
+    finally:
+        dist.destroy_process_group()
+
+
 @pytest.mark.parametrize("loopback", [False, True])
 def test_owner_merge_hot_entities(hiplib, loopback):
     """Owner mode (world size 1, RCCL) on a table large enough for compact
