@@ -352,8 +352,11 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
         rrs[colu[u]] = colu[u] < k ? A.rel.row(pr)[colu[u]] : 0.f;
       }
   }
+  // (no barrier: phv / ptv are already in every lane -- tr2_col_sum gives
+  // them the same bits -- and the LDS copies are read after later barriers)
   float rr[2];
-  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u) rr[u] = (has(u) && colu[u] < k) ? A.rel.row(pr)[colu[u]] : 0.f;
   auto load_rows = [&]() {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -362,7 +365,6 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
       rr[u] = has(u) ? rrs[colu[u]] : 0.f;
     }
   };
-  load_rows();
   // element (row, column tile u): projected x / y rows; scored x = xp + r, y = yp
   // (p = the row's own projected value; the positive's own row is t)
   auto xyp = [&](int u, float p, bool own_y, float& xp, float& yp) {
@@ -667,7 +669,8 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
     }
 
     KGE_PROF(38);
-    __syncthreads();   // (X is dead since GEMM1) the positive-side slices over it
+    // (no barrier: X is dead since GEMM1, several barriers ago; the row vectors
+    // written above are read by GEMM2, after the barrier that ends the staging)
     KGE_PROF(39);
     load_rows();
     // ---- Q rows: negative q's positive-side slice -> GEMM2's norms
