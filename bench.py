@@ -253,7 +253,7 @@ def accounting(w, B, K, d, E, R, batch):
     # TransR: three products per positive: P = X M (K+2 rows), S M^T (2K+4
     # slice rows: every slice's ||M g||^2 is a clip_by_norm term), X^T S' (K+2)
     flops = 2.0 * d * d * (4 * K + 8) * B
-    return {"bound": "mfma", "step_flops": flops, "kernels": {"transr_kernel": flops},
+    return {"bound": "mfma", "step_flops": flops, "kernels": {"transr2_kernel": flops},
             "survey_flops": 6.0 * d * d * (K + 2) * B}
 
 
@@ -416,19 +416,36 @@ def cpu_baseline(triples, E, R, B, K, d, budget_s):
                       % (n, B, K, d, threads, t, n1, t1)}
 
 
+def _round_key(name):
+    """profiles/ run directories in build order: r05b < r05z < r05aa < r06."""
+    import re
+    m = re.match(r"r(\d+)([a-z]*)$", name)
+    return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else None
+
+
 def pmc_traffic(workload):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    --pmc summary (tools/pmc_traffic.py), or None. NOT measured in this run:
-    the counters need their own rocprofv3 --pmc pass; the line names the file
-    (``traffic_source``)."""
-    name = "pmc_traffic.json" if workload == "c2" else "pmc_traffic_%s.json" % workload
+    """HBM bytes per launch of the leg's kernels from the newest committed
+    rocprofv3 --pmc summary, profiles/<run>/pmc_traffic_<workload>.json
+    (tools/pmc_traffic.py; <run> = r<round><suffix>, newest by round then
+    suffix), or None. NOT measured in this run: the counters need their own
+    rocprofv3 --pmc pass; the line names the file (``traffic_source``)."""
+    pdir = os.path.join(ROOT, "profiles")
+    name = "pmc_traffic_%s.json" % workload
     try:
-        with open(os.path.join(ROOT, "profiles", name)) as f:
+        runs = sorted((d for d in os.listdir(pdir) if _round_key(d) and os.path.exists(os.path.join(pdir, d, name))),
+                      key=_round_key)
+    except OSError:
+        return None
+    if not runs:
+        return None
+    rel = "profiles/%s/%s" % (runs[-1], name)
+    try:
+        with open(os.path.join(ROOT, rel)) as f:
             out = json.load(f)
-        out["_source"] = "profiles/%s (rocprofv3 --pmc, committed; not this run)" % name
-        return out
     except (OSError, ValueError):
         return None
+    out["_source"] = "%s (rocprofv3 --pmc, committed; not this run)" % rel
+    return out
 
 
 # ---------------------------------------------------------------- entry-point legs
@@ -748,8 +765,11 @@ def main():
     else:
         dom = names[0]
         tf = acc["kernels"][dom] / (ks * 1e-3) / 1e12
+        pmc = pmc_traffic(args.workload)
+        traffic = (pmc or {}).get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
         roof = {"bound": "mfma", "kernel": dom, "achieved": round(tf, 2), "peak": F32_MFMA_PEAK_TF,
-                "unit": "TFLOP/s", "frac": round(tf / F32_MFMA_PEAK_TF, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(tf / F32_MFMA_PEAK_TF, 4), "traffic": traffic,
+                "traffic_source": pmc["_source"] if traffic is not None else None,
                 "flops_per_launch": acc["kernels"][dom], "survey_flops_per_step": acc["survey_flops"],
                 "step": {"ms_per_step": round(ms, 5), "achieved": round(acc["step_flops"] / (ms * 1e-3) / 1e12, 2)},
                 "kernels": {dom: {"ms": round(ks, 5)}, "update+apply": {"ms": round(ku, 5)},

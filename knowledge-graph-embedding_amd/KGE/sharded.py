@@ -70,8 +70,12 @@ class Exchange:
     gloo group given device tensors stages them through host memory (the
     multi-process tests that put several ranks on one GPU)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, force=False):
+        """``force``: issue every collective even on a one-rank group (the
+        RCCL tensor forms then run as copies -- a one-GPU test of the N-rank
+        code path)."""
         self.group = group
+        self.force = bool(force)
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.tensor_forms = dist.get_backend(group) == "nccl"
@@ -89,7 +93,7 @@ class Exchange:
             full.copy_(f)
 
     def all_reduce(self, t):
-        if self.world == 1:   # (one rank: the sum is the tensor itself)
+        if self.world == 1 and not self.force:   # (one rank: the sum is the tensor itself)
             return
         h = self._host(t)
         dist.all_reduce(h, group=self.group)
@@ -107,7 +111,7 @@ class ShardedStep:
     """Drop-in for ``FusedStep`` across G ranks (see module docstring)."""
 
     def __init__(self, model, exchange=None, mode="auto", local_fast=True, loopback=False, capacity_slack=1.1,
-                 capacity_floor=1024, batch_hint=None, optimizer=None):
+                 capacity_floor=1024, batch_hint=None, optimizer=None, force_collectives=False):
         """``loopback`` (sparse mode): own ids too go through the exchange blocks
         (a one-GPU rehearsal of the remote path). Each owner block holds
         ceil(capacity_slack * occurrences / G) + capacity_floor rows; a step
@@ -124,11 +128,17 @@ class ShardedStep:
         buffers for both passes up front, so an Adam step falling through to
         the row exchange never re-plans a second copy of the shard. The owner
         pass's key capacity follows ``capacity_slack`` / ``capacity_floor``
-        too (at least 5/4 of the expected owned negatives + 4096)."""
+        too (at least 5/4 of the expected owned negatives + 4096).
+        ``force_collectives``: take the N-rank code path (separate send /
+        receive buffers, every collective issued) even on one rank -- the
+        RCCL world-1 tests' way to run the tensor-form collectives."""
         self.model = model
         self.ex = exchange or Exchange()
+        if force_collectives:
+            self.ex.force = True
         G, g = self.ex.world, self.ex.rank
         self.G, self.g = G, g
+        self.multi = G > 1 or self.ex.force   # the N-rank code path
         t = model._fused_tables()
         self.tables = t
         self.names = engine.fused_names(model)
@@ -207,9 +217,10 @@ class ShardedStep:
         self.norm2 = self.red[o:o + 4]
         self.loss = self.red[o + 4:o + 5]
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
-        # sticky exchange-overflow flag: the max of every step's all-reduced
-        # flag since check_status() last read it (no host sync per step)
-        self.xerr = torch.zeros(1, dtype=torch.float32, device=dev)
+        # sticky overflow flags [exchange block, owner pass]: the max of every
+        # step's all-reduced flags since check_status() last read them (no host
+        # sync per step)
+        self.xerr = torch.zeros(2, dtype=torch.float32, device=dev)
         c = getattr(model, "constraint", False)
         self.renorm = self.mid in _RENORM and bool(c)
         self.clip = self.mid in _CLIP and bool(c)
@@ -238,7 +249,7 @@ class ShardedStep:
         # one rank: every row is local, so the fused single-device step runs on
         # the shard itself (in-kernel SGD, compact update launch) -- no cache
         self.direct = None
-        if self.fused is not None and G == 1 and mode != "dense" and local_fast and not self.loopback:
+        if self.fused is not None and not self.multi and mode != "dense" and local_fast and not self.loopback:
             td = dict(t)
             td["ent"] = self.shard[:, :self.ce].view(self.ent_shape)
             if self.ca:
@@ -574,7 +585,7 @@ class ShardedStep:
                 for k in ("req_ids", "recv_ids"):
                     if k in old:
                         old[k] = torch.zeros(old[k].shape[0], dtype=idx_dtype, device=self.device)
-                if G == 1:
+                if not self.multi:
                     old["recv_ids"] = old["req_ids"]
                 old["dtype"] = idx_dtype
             return old
@@ -582,7 +593,7 @@ class ShardedStep:
         if old is not None:   # (re-planned: keep what the other pass sized for)
             n_occ = max(n_occ, old["n_occ"])
             pos_rows = max(pos_rows, old["pos_rows"])
-        remote = G > 1 or self.loopback or self._needs_loop
+        remote = self.multi or self.loopback or self._needs_loop
         cap = max(1, int(math.ceil(self.slack * n_occ / G)) + self.cap_floor) if remote else 1
         rows = self.Es + G * cap + pos_rows
         if dev.type == "cuda" and rows * C * 4 > (1 << 32):
@@ -612,7 +623,7 @@ class ShardedStep:
              "err": zero[hs * 8 + zb:hs * 8 + zb + 4].view(torch.float32),
              # [exchange plan's flag | owner pass's flag], zeroed with the rest
              "errs": zero[hs * 8 + zb:hs * 8 + zb + 8].view(torch.float32)}
-        if G > 1:
+        if self.multi:
             b["recv_cnt"] = torch.zeros(G, dtype=torch.int32, device=dev)
             b["recv_ids"] = torch.zeros(G * cap, dtype=idx_dtype, device=dev)
             b["send"] = torch.zeros(G * cap, C, dtype=torch.float32, device=dev)
@@ -672,7 +683,7 @@ class ShardedStep:
         n_neg = int(neg.shape[0])
         split = self.mid in _SPLIT and is_train and isinstance(optimizer, _opt.SGD)
         loop = self.loopback or not split
-        if loop and not self.loopback and G == 1 and (self._ext is None or self._ext["cap"] == 1):
+        if loop and not self.loopback and not self.multi and (self._ext is None or self._ext["cap"] == 1):
             self._needs_loop = True    # a one-rank gradient-mode step needs the blocks
             if self._ext is not None:
                 self._ext["n_occ"] = -1   # re-plan the blocks
@@ -700,7 +711,7 @@ class ShardedStep:
         _hip.check(self.lib.kge_exchange_plan(ctypes.byref(x), st), "kge_exchange_plan")
         # 2. requests to the owners, owners gather, rows back
         blocks = ext[self.Es:b["pos_base"]]
-        if G > 1:
+        if self.multi:
             self.ex.all_to_all(b["recv_cnt"], b["req_cnt"])
             self.ex.all_to_all(b["recv_ids"], b["req_ids"])
             self._xrows(b, _hip.XROWS_GATHER, b["send"], C, self.shard)
@@ -708,7 +719,10 @@ class ShardedStep:
         elif loop:
             self._xrows(b, _hip.XROWS_GATHER, blocks, C, self.shard)
         lt = self._local_tables(ext)
-        small = self.red[-8:]     # [norm^2 x4 | loss | - | - | exchange error flag]
+        # [norm^2 x4 | loss | exchange flag | owner flag | any flag]: summed
+        # across ranks, each slot counts the ranks that raised its flag (the
+        # kernels' abort word is the last)
+        small = self.red[-8:]
         if split:
             # 3a. score pass, global norms / loss / error, update pass
             # (prof_events [before K0, before KS, after KS, after KU]: the
@@ -724,15 +738,16 @@ class ShardedStep:
             f.tables = lt
             f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_PHASE_SCORE
             f(lpos, True, optimizer, neg_ids=lneg, prof_events=ev_s)
-            small[-1:].copy_(b["err"])
-            if G > 1:
+            small[5:7].copy_(b["errs"])   # (no owner pass: its flag stays 0)
+            small[7:8].copy_(b["err"])
+            if self.multi:
                 self.ex.all_reduce(small)
-            torch.maximum(self.xerr, small[-1:], out=self.xerr)
+            torch.maximum(self.xerr, small[5:7], out=self.xerr)
             f.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_PHASE_UPDATE
             f.remote_from = self.Es
             f.abort = small[-1:]
             f(lpos, True, optimizer, neg_ids=lneg, prof_events=ev_u)
-            if G > 1:
+            if self.multi:
                 self.ex.all_reduce(self.red[:-8])   # relation gradients
             grad_blocks = [blocks]
         else:
@@ -744,10 +759,11 @@ class ShardedStep:
                 ([gb[1]] if self.ca else [])
             f.grad_row_offset = self.Es   # the step addresses rows >= Es only (all ids through the blocks)
             f(lpos, is_train, optimizer if is_train else None, neg_ids=lneg, prof_events=prof_events)
-            small[-1:].copy_(b["err"])
-            if G > 1:
+            small[5:7].copy_(b["errs"])
+            small[7:8].copy_(b["err"])
+            if self.multi:
                 self.ex.all_reduce(self.red)
-            torch.maximum(self.xerr, small[-1:], out=self.xerr)
+            torch.maximum(self.xerr, small[5:7], out=self.xerr)
             grad_blocks = gb
         if not is_train:
             return self.loss
@@ -755,10 +771,10 @@ class ShardedStep:
         # them source by source in rank order (SGD) or add them up (Adam: a
         # dense keras Adam of the shard)
         dense_items = []
-        if G > 1 or loop:
+        if self.multi or loop:
             adam = isinstance(optimizer, _opt.Adam)
             for k, gk in enumerate(grad_blocks):
-                if G > 1:
+                if self.multi:
                     r = b["send"] if gk.shape[1] == C else torch.empty_like(gk)
                     self.ex.all_to_all(r, gk)
                     gk = r
@@ -824,7 +840,7 @@ class ShardedStep:
             raise RuntimeError("owner-side scoring: " + self.lib.kge_last_error().decode(errors="replace"))
         o["R"] = R
         o["rec"] = torch.zeros(G * Bn, R, dtype=torch.float32, device=dev)
-        o["rec_in"] = torch.zeros(G * Bn, R, dtype=torch.float32, device=dev) if G > 1 else o["rec"]
+        o["rec_in"] = torch.zeros(G * Bn, R, dtype=torch.float32, device=dev) if self.multi else o["rec"]
         o["stats_mine"] = o["stats"][g * Bn:(g + 1) * Bn]
         fo.owner["records"] = o["rec"]
         fm.owner = dict(common, records=o["rec_in"], stats_out=o["stats_mine"])
@@ -903,7 +919,7 @@ class ShardedStep:
         x.pos = x.neg = batch.data_ptr()
         _hip.check(self.lib.kge_exchange_plan(ctypes.byref(x), st), "kge_exchange_plan")
         blocks = ext[self.Es:b["pos_base"]]
-        if G > 1:
+        if self.multi:
             ex.all_to_all(b["recv_cnt"], b["req_cnt"])
             ex.all_to_all(b["recv_ids"], b["req_ids"])
             self._xrows(b, _hip.XROWS_GATHER, b["send"], C, self.shard)
@@ -916,7 +932,7 @@ class ShardedStep:
         # (gathered straight into P: the source rows [0, pos_base) and P do not overlap)
         torch.index_select(ext[:b["pos_base"]], 0, lpos[:, 0::2].reshape(-1).to(torch.int64), out=mine)
         gtrip = o["gtrip"]
-        if G > 1:   # (one rank: P is `mine`, the virtual batch is the batch)
+        if self.multi:   # (one rank: P is `mine`, the virtual batch is the batch)
             ex.all_gather(P, mine)
             ex.all_gather(gtrip, batch)
         else:
@@ -946,19 +962,20 @@ class ShardedStep:
             fo.flags, fo.abort = f_os, None
             fo(gtrip, is_train, opt, neg_ids=o["gneg"], prof_events=ev_s)
         # 4. records to the positives' ranks; 5. merge
-        if G > 1:
+        if self.multi:
             ex.all_to_all(o["rec_in"], o["rec"])
         if fast:
             self._owner_run(o, fm, lpos, is_train, opt, f_ms)
         else:
             fm.flags, fm.abort = f_ms, None
             fm(lpos, is_train, opt)
-        # 6. [norm^2 x4 | loss | - | - | error flag], the stats
-        torch.amax(b["errs"], dim=0, keepdim=True, out=small[-1:])
-        if G > 1:
+        # 6. [norm^2 x4 | loss | exchange flag | owner flag | any flag], the stats
+        small[5:7].copy_(b["errs"])
+        torch.sum(b["errs"], dim=0, keepdim=True, out=small[7:8])
+        if self.multi:
             ex.all_reduce(small)
             ex.all_gather(o["stats"], o["stats_mine"])
-        torch.maximum(self.xerr, small[-1:], out=self.xerr)
+        torch.maximum(self.xerr, small[5:7], out=self.xerr)
         if not is_train:
             return self.loss
         # 7. the owned negatives' rows, then 8. the positives' rows
@@ -973,11 +990,11 @@ class ShardedStep:
             fm.flags, fm.abort = f_mu, small[-1:]
             fm(lpos, True, optimizer)
         # 9. relation gradients; the fetched rows' gradients back to their owners
-        if G > 1:
+        if self.multi:
             ex.all_reduce(self.red[:-8])
-        if G > 1 or loop:
+        if self.multi or loop:
             gk = blocks
-            if G > 1:
+            if self.multi:
                 ex.all_to_all(b["send"], blocks)
                 gk = b["send"]
             for src in range(G):
@@ -1260,11 +1277,11 @@ class ShardedStep:
         if self.fused is not None:
             _hip.check_device_status(self.status, "kge_step")
         if self._ext is not None:
-            x = float(self.xerr)
-            if x == 0.0:
+            xf, of = self.xerr.tolist()
+            if xf == 0.0 and of == 0.0:
                 return
             self.xerr.zero_()
-            if x >= 2.0:   # (the owner pass's flag, kge_hip.h owner_err)
+            if of != 0.0:   # (the owner pass's flag, kge_hip.h owner_err)
                 raise RuntimeError("owner-side scoring: this rank's owned negatives overflowed the owner pass's "
                                    "%d key positions; the step was skipped on every rank -- raise capacity_slack "
                                    "or capacity_floor" % (self._own or {}).get("key_cap", 0))

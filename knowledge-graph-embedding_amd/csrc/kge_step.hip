@@ -245,6 +245,9 @@ __global__ __launch_bounds__(256) void merge_plan_kernel(StepArgs A, float* zero
       set_status(A.status, KGE_EWORKSPACE);
     }
   }
+  // another plan's workspace: nothing of it is touched (this plan's own
+  // refused pass may still rank its keys: the chunk kernels refuse it)
+  if (ws_refused(A.ctl, A.sig, A.status, nullptr)) return;
   // the keys the merge left (seg_raw, in positive order), staged whole; each
   // wave ranks 4 of them, its lanes sweeping n / 64 keys each
   const int n = 3 * (int)A.B;

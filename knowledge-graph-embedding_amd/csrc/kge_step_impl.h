@@ -48,6 +48,11 @@
 #ifndef KGE_GUARD_KU
 #define KGE_GUARD_KU 1      // update kernel: workspace plan guard at entry (tuning / A-B knob)
 #endif
+#ifndef KGE_FILE_EARLY
+#define KGE_FILE_EARLY 0    // score kernel: negatives' keys filed during the stream (1: claims after the first
+                            // batch's loads, stored after its compute; 2: claims after the stream, stored after
+                            // the merge barrier; 0: in the finalise pass) (A-B knob)
+#endif
 #ifndef KGE_UPDATE_U
 #define KGE_UPDATE_U 8      // update kernel: list entries in flight per wave at NC = 1 (tuning knob)
 #endif
@@ -138,37 +143,58 @@ __device__ __forceinline__ float neg_coef(const StepArgs& A, float s, float sp, 
 // positives' keys first (they hold the longest lists -- relation rows,
 // skewed entities -- which then start early instead of forming the update
 // launch's tail), then the negatives'
-__device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_t code, uint32_t kpos_own = ~0u) {
-  uint32_t r;
-  int64_t li = dest;   // list index
+struct KeyClaim {
+  uint32_t r;   // list position the key took
+  uint32_t h;   // compact launches: its hash slot
+};
+// the returning half of bin_key: the destination's counter (or hash slot)
+// taken. Non-compact: one atomic whose result is only needed by bin_commit,
+// so the two can be issued apart (the score kernel's early filing)
+__device__ __forceinline__ KeyClaim bin_claim(const StepArgs& A, int64_t dest) {
+  KeyClaim c;
   if (A.compact) {
     const unsigned long long key = (unsigned long long)((uint32_t)dest + 1u) << 32;
     uint32_t h = ((uint32_t)dest * 2654435761u) >> A.hshift;
     for (;;) {   // at most one pass: the table has >= 2x as many slots as keys
       const unsigned long long cur = atomicCAS(&A.htab[h], 0ull, key | 1ull);
-      if (cur == 0ull) { r = 0u; break; }
-      if ((cur & 0xFFFFFFFF00000000ull) == key) { r = (uint32_t)atomicAdd(&A.htab[h], 1ull); break; }
+      if (cur == 0ull) { c.r = 0u; break; }
+      if ((cur & 0xFFFFFFFF00000000ull) == key) { c.r = (uint32_t)atomicAdd(&A.htab[h], 1ull); break; }
       h = (h + 1u) & A.hmask;
     }
-    li = h;
+    c.h = h;
+  } else {
+    c.r = atomicAdd(&A.cnt[dest], 1u);
+    c.h = 0u;
+  }
+  return c;
+}
+// the storing half: the code into the destination's list at the claimed
+// position (the overflow list past capacity); compact launches also record
+// the key's leader-table entry
+__device__ __forceinline__ void bin_commit(const StepArgs& A, int64_t dest, uint32_t code, KeyClaim c,
+                                           uint32_t kpos_own = ~0u) {
+  int64_t li = dest;   // list index
+  if (A.compact) {
+    li = c.h;
     // (the owner pass hands each key its position in the workgroup's block)
     const uint32_t kpos = kpos_own != ~0u ? kpos_own
         : code < A.nkeyneg
         ? A.npos3 + (code >> A.kshift) * (uint32_t)A.Keff + (code & ((1u << A.kshift) - 1u))
         : 3u * ((code - A.nkeyneg) >> 2) + ((code - A.nkeyneg) & 3u);
-    A.leaders[kpos] = make_uint4((uint32_t)dest, r == 0u ? code : 0xFFFFFFFFu, h, 0u);
+    A.leaders[kpos] = make_uint4((uint32_t)dest, c.r == 0u ? code : 0xFFFFFFFFu, c.h, 0u);
     // position 0's code is the leader table's (a 50M-row table's destinations
     // mostly hold one key: no scattered list store for them at all)
-    if (KGE_COMPACT_LIST0 && r == 0u) return;
-  } else {
-    r = atomicAdd(&A.cnt[dest], 1u);
+    if (KGE_COMPACT_LIST0 && c.r == 0u) return;
   }
-  if (r < (uint32_t)A.cap) {
-    A.list[li * A.cap + r] = code;
+  if (c.r < (uint32_t)A.cap) {
+    A.list[li * A.cap + c.r] = code;
   } else {
     const uint32_t o = atomicAdd(&A.ctl->ovf_count, 1u);
     A.ovf[o] = ((uint64_t)dest << 32) | code;
   }
+}
+__device__ __forceinline__ void bin_key(const StepArgs& A, int64_t dest, uint32_t code, uint32_t kpos_own = ~0u) {
+  bin_commit(A, dest, code, bin_claim(A, dest), kpos_own);
 }
 
 // global entity id -> its row of the step's entity table, range-checked:
@@ -1042,7 +1068,11 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
         // every workgroup's keys are filed: hand the overflow length to the
         // update kernel and restart the overflow list for the next step
         A.ctl->ovf_len = __hip_atomic_exchange(&A.ctl->ovf_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (A.mark_pending) A.ctl->score_pending = A.sig;   // the phase gate's token (kge_abi.hip)
+        // the phase gate's token (kge_abi.hip): set by a PHASE_SCORE pass,
+        // cleared by any other score pass of the plan (a full step consumes
+        // the lists a pending update pass would have read)
+        __hip_atomic_store(&A.ctl->score_pending, A.mark_pending ? A.sig : 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       } else {
         A.ctl->scale[tid - 1] = -A.lr * (A.clip_norm / fmaxf(sqrtf(s), A.clip_norm));
         if (A.norm2_out) A.norm2_out[tid - 1] = s;

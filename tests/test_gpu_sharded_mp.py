@@ -177,3 +177,66 @@ def test_two_ranks_one_gpu_owner_bench_shape(hiplib):
         assert abs(got_losses[s] - ref["loss"]) <= 1e-5 * max(1.0, abs(ref["loss"])), s
     for k, v in ref_w.items():
         np.testing.assert_allclose(got[k], v, atol=1e-5, err_msg=k)
+
+
+def _overflow_worker(rank, port, mode, out):
+    import torch.distributed as dist
+    import __graft_entry__  # noqa: F401
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=2)
+    from KGE import loss, optimizers, score
+    from KGE.models.translating_based.TransE import TransE
+    from KGE.ns_strategy import UniformStrategy
+    from KGE.sharded import ShardedStep
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(91)
+    E_, R_, d_, B_, K_ = 4000, 5, 24, 32, 4
+    W = {"ent_emb": rng.uniform(-0.3, 0.3, (E_, d_)).astype(np.float32),
+         "rel_emb": rng.uniform(-0.3, 0.3, (R_, d_)).astype(np.float32)}
+    m = TransE({"embedding_size": d_}, K_, "h+t", score_fn=score.LpDistance(2),
+               loss_fn=loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
+               ns_strategy=UniformStrategy(np.arange(E_), seed=3), constraint=False)
+    m.metadata = {"ind2ent": list(range(E_)), "ind2rel": list(range(R_))}
+    m.model_weights = {k: torch.tensor(v, device=dev) for k, v in W.items()}
+    # blocks of a few rows: both ranks' steps request far more remote rows
+    st = ShardedStep(m, mode=mode, batch_hint=B_, capacity_slack=0.05, capacity_floor=0,
+                     optimizer=optimizers.SGD(0.05))
+    pos = np.stack([rng.integers(0, E_, B_), rng.integers(0, R_, B_), rng.integers(0, E_, B_)], 1)
+    st(torch.tensor(pos, device=dev), True, optimizers.SGD(0.05))
+    torch.cuda.synchronize()
+    msg = ""
+    try:
+        st.check_status()
+    except RuntimeError as e:
+        msg = str(e)
+    st.sync()
+    unchanged = bool(np.array_equal(m.model_weights["ent_emb"].cpu().numpy(), W["ent_emb"]))
+    out.put((rank, msg, unchanged))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["sparse", "owner"])
+def test_two_ranks_both_overflow_exchange(hiplib, mode):
+    """Both ranks overflow an exchange block in the same step: the step is
+    void on both (no table row changes) and check_status() names the
+    exchange block on both -- the per-kind flags are summed across ranks in
+    their own slots, so two exchange overflows are not read as the owner
+    pass's key overflow."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_overflow_worker, args=(r, port, mode, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    try:
+        res = [q.get(timeout=100) for _ in range(2)]
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.exitcode is None:
+                p.kill()
+    for p in ps:
+        assert p.exitcode == 0
+    for rank, msg, unchanged in res:
+        assert "overflowed an owner block" in msg, (rank, msg)
+        assert unchanged, rank

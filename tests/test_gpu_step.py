@@ -835,6 +835,13 @@ def test_update_phase_needs_its_score_pass(hiplib):
     after = m.model_weights["ent_emb"].clone()
     assert run(U) == _hip.KGE_EWORKSPACE             # a second update pass
     assert torch.equal(m.model_weights["ent_emb"], after)
+    # a full (non-split) step of the same plan between the passes consumes the
+    # score pass's lists and clears its token: the update pass after it is refused
+    ws.zero_()
+    assert run(S) == _hip.KGE_OK and run(0) == _hip.KGE_OK
+    after = m.model_weights["ent_emb"].clone()
+    assert run(U) == _hip.KGE_EWORKSPACE
+    assert torch.equal(m.model_weights["ent_emb"], after)
 
 
 def test_hinge_zero_negatives_is_nan(hiplib):
@@ -1021,7 +1028,10 @@ def test_fused_adam_three_steps(hiplib, model_name, constraint):
                          + [("dense", "RESCAL", None), ("dense", "TransH", "lppow2")]
                          + [(m, n, s) for m in ("owner", "owner-loopback")
                             for n, s in (("TransE", "lp2"), ("RotatE", "lp1"), ("DistMult", None),
-                                         ("TransE", "lpinf"), ("TransE", "lp3"))])
+                                         ("TransE", "lpinf"), ("TransE", "lp3"))]
+                         + [(m, n, s) for m in ("sparse-forced", "dense-forced", "owner-forced")
+                            for n, s in (("TransE", "lp2"), ("RotatE", "lp1"))]
+                         + [("sparse-forced", "TransD", "lppow2"), ("dense-forced", "RESCAL", None)])
 def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
     """KGE/sharded.py on the RCCL backend (world size 1): e mod G shard,
     kge_sample draws, the device sparse exchange (kge_exchange_plan ->
@@ -1031,7 +1041,9 @@ def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
     (grad-mode step, one all-reduce, kge_apply), or owner-side scoring (the
     owner pass over the virtual batch with in-kernel draws, records, merge,
     owner update then the positives' rows); two steps == two oracle steps
-    with the same draws."""
+    with the same draws. "-forced": the N-rank code path on the one rank
+    (force_collectives: separate send / receive buffers, every all_to_all /
+    all_gather / all_reduce issued as an RCCL tensor-form call)."""
     import torch.distributed as dist
     from KGE import loss, optimizers, score
     from KGE.ns_strategy import UniformStrategy
@@ -1050,9 +1062,12 @@ def test_sharded_step_world1_rccl(hiplib, mode, model_name, score_kind):
         m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
         # "sparse" forces the exchange + row cache even on one rank; "local" is
         # the one-rank shortcut (the fused step directly on the shard)
-        st = ShardedStep(m, mode="dense" if mode == "dense" else "owner" if mode.startswith("owner") else "sparse",
-                         local_fast=mode == "local", loopback=mode.endswith("loopback"))
+        forced = mode.endswith("-forced")
+        st = ShardedStep(m, mode="dense" if mode.startswith("dense") else "owner" if mode.startswith("owner")
+                         else "sparse", local_fast=mode == "local", loopback=mode.endswith("loopback"),
+                         force_collectives=forced)
         assert (st.direct is not None) == (mode == "local")
+        assert st.multi == forced
         ref_w = W
         opt = optimizers.SGD(0.05)
         for it in range(2):
@@ -1316,6 +1331,16 @@ def test_owner_update_phase_needs_its_score_pass(hiplib):
         torch.cuda.synchronize()
         assert int(st.status.item()) == _hip.KGE_EWORKSPACE
         assert torch.equal(st.shard, shard)
+        # the merge's update pass (the segmented sum) gates itself the same way
+        fm = o["fm"]
+        fm.workspace.zero_()
+        fm.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER_MERGE | _hip.FLAG_PHASE_UPDATE
+        fm.abort = None
+        st.status.zero_()
+        fm(o["lpos"], True, opt)
+        torch.cuda.synchronize()
+        assert int(st.status.item()) == _hip.KGE_EWORKSPACE
+        assert torch.equal(st.shard, shard)
     finally:
         dist.destroy_process_group()
 
@@ -1324,11 +1349,12 @@ def test_owner_update_phase_needs_its_score_pass(hiplib):
 def test_owner_merge_hot_entities(hiplib, loopback):
     """Owner mode (world size 1, RCCL) on a table large enough for compact
     launches, with Zipf-like hot rows among the positives: 40 % of the heads
-    are entity 7, 30 % of the tails entity 11, 60 % of the relations 0. The
-    merge's update pass hands the long destinations to long_rows_kernel and
-    the relation rows to rel_seg_kernel; two steps == two oracle steps, and
-    == (up to summation order) the same steps with the relation rows summed
-    by the update kernel itself (KGE_FLAG_DEBUG_NO_REL_SEG)."""
+    are entity 7, 30 % of the tails entity 11, 60 % of the relations 0. At
+    3 B <= 8192 keys the merge's update pass is the segmented sum
+    (merge_plan / merge_chunk / merge_combine kernels); two steps == two
+    oracle steps, and == (up to summation order) the same steps with every
+    destination summed by the update kernel itself (KGE_FLAG_DEBUG_NO_REL_SEG).
+    test_owner_merge_fallback_update covers the larger batches' path."""
     import torch.distributed as dist
     from KGE import _hip, loss, optimizers, score
     from KGE.ns_strategy import UniformStrategy
@@ -1369,6 +1395,70 @@ def test_owner_merge_hot_entities(hiplib, loopback):
             del st
         for kk in outs[0]:   # (rel_seg adds four row groups' partials: equal up to summation order)
             np.testing.assert_allclose(outs[0][kk], outs[1][kk], rtol=0, atol=1e-6, err_msg=kk)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_owner_merge_fallback_update(hiplib):
+    """Owner mode with 3 B > 8192 positive keys (B = 2800): the merge's update
+    pass falls back to the update kernel with long destinations deferred to
+    long_rows_kernel and relation rows summed by rel_seg_kernel (Zipf-hot
+    heads / relation). A step whose exchange blocks overflow is void and
+    leaves every relation gradient row zero (rel_seg_kernel's abort path:
+    never the previous values); then two clean steps == two oracle steps."""
+    import torch.distributed as dist
+    from KGE import loss, optimizers, score
+    from KGE.ns_strategy import UniformStrategy
+    from KGE.sharded import ShardedStep
+    dev = _dev()
+    _init_world1(dist, dev)
+    try:
+        E, R, d, B, K = 100000, 6, 24, 2800, 4
+        W = _weights("TransE", E, R, d, np.random.default_rng(27))
+        rng = np.random.default_rng(28)
+
+        def batch():
+            h = np.where(rng.random(B) < 0.3, 7, rng.integers(0, E, B))
+            t = rng.integers(0, E, B)
+            r = np.where(rng.random(B) < 0.6, 0, rng.integers(0, R, B))
+            return np.stack([h, r, t], 1).astype(np.int64)
+
+        def model():
+            m = _make("TransE", d, K, "h+t", score.LpDistance(2), loss.SelfAdversarialNegativeSamplingLoss(3.0, 1.0),
+                      E, R, UniformStrategy(np.arange(E), seed=8), constraint=False)
+            m.model_weights = {kk: torch.tensor(v, device=dev) for kk, v in W.items()}
+            return m
+        opt = optimizers.SGD(0.05)
+        # the void step: every positive row through 280-row blocks (loopback)
+        m = model()
+        st = ShardedStep(m, mode="owner", loopback=True, local_fast=False, capacity_slack=0.05, capacity_floor=0)
+        st.grel["rel"].fill_(7.0)
+        st(torch.tensor(batch(), device=dev), True, opt)
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError, match="overflowed an owner block"):
+            st.check_status()
+        assert float(st.grel["rel"].abs().max()) == 0.0
+        st.sync()
+        for kk, v in W.items():
+            np.testing.assert_array_equal(m.model_weights[kk].cpu().numpy(), v, err_msg=kk)
+        del st
+        m = model()
+        st = ShardedStep(m, mode="owner", local_fast=False)
+        ref_w = W
+        for it in range(2):
+            pos = batch()
+            plane = m.ns_strategy.offset
+            lv = float(st(torch.tensor(pos, device=dev), True, opt))
+            torch.cuda.synchronize()
+            st.check_status()
+            neg = orc.negatives(pos, K, "h+t", E, seed=8, plane=plane)
+            ref = orc.train_step("TransE", ref_w, pos, neg, score=("lp", 2.0), loss=("sans", 3.0, 1.0), lr=0.05,
+                                 constraint=False)
+            ref_w = ref["weights"]
+            assert abs(lv - ref["loss"]) <= TOL * max(1.0, abs(ref["loss"])), it
+        st.sync()
+        for kk, v in ref_w.items():
+            np.testing.assert_allclose(m.model_weights[kk].cpu().numpy(), v, atol=TOL, err_msg=kk)
     finally:
         dist.destroy_process_group()
 

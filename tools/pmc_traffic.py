@@ -16,7 +16,8 @@ import sys
 from collections import defaultdict
 
 KERNELS = ("score_kernel", "update_kernel", "constrain_rows_kernel", "apply_kernel", "rel_item_kernel", "rel_dr_kernel",
-           "rescal_apply_kernel", "transr_kernel", "transr_proj_apply")
+           "rescal_apply_kernel", "transr2_kernel", "transr_kernel", "transr_proj_apply", "rescal_norms_kernel",
+           "owner_merge_kernel", "owner_coef_kernel", "merge_chunk_kernel")
 
 
 def short(name):
