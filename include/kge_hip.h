@@ -181,10 +181,14 @@ enum {
    *       update pass (remote_rows_from, relation gradients to grad_out[1]). */
   KGE_FLAG_OWNER = 128,
   KGE_FLAG_OWNER_MERGE = 256,
-  KGE_FLAG_DEBUG_NO_REL_SEG = 512   /* test hook: the owner merge's update pass sums the
+  KGE_FLAG_DEBUG_NO_REL_SEG = 512,  /* test hook: the owner merge's update pass sums the
                                        relation rows in the update kernel (one wave per
                                        relation) instead of the per-relation segment pass
                                        (same sums up to their order) */
+  KGE_FLAG_SCORE_CLASSIC = 1024     /* test / A-B hook: the one-generation score kernel
+                                       (every positive's workgroup resident at once)
+                                       instead of the pipelined one (TransE, rows of
+                                       <= 256 floats); same values up to summation order */
 };
 
 typedef struct kge_table {

@@ -28,6 +28,7 @@ FLAG_PHASE_UPDATE = 64
 FLAG_OWNER = 128
 FLAG_OWNER_MERGE = 256
 FLAG_DEBUG_NO_REL_SEG = 512   # test hook: relation rows in the update kernel (compact launches)
+FLAG_SCORE_CLASSIC = 1024     # test / A-B hook: the one-generation score kernel, not the pipelined one
 RANK_TRANS, RANK_ROT, RANK_MUL, RANK_DOT = range(4)
 RANK_FLAG_LANE_PASS = 1
 RPROJ_NONE, RPROJ_HYPER, RPROJ_RANK1 = range(3)

@@ -219,6 +219,10 @@ struct StepArgs {
   int32_t nP;       // positives per score workgroup = kStepWaves / wpp
   int32_t SW;       // negative slots per wave
   int32_t nWG;      // score workgroups
+  // pipelined score kernel (kge_score_pipe.h): a run of pipe_ppw positives
+  // per 16-wave workgroup, pipe_sw negative slots per wave per positive
+  bool pipe = false;
+  int32_t pipe_ppw = 0, pipe_sw = 0;
   int32_t cap;      // destination list capacity (entries per destination)
   int32_t snap_cols, gcols, rel_gcols;
   uint32_t nkeyneg; // B << kshift: codes below are negatives (i << kshift | j), above positive rows (+4i+c)
@@ -282,6 +286,8 @@ struct StepGeom {
   int vec, nc;
   int nWG, gridU;
   size_t lds_score;
+  int nWG_pipe = 0;        // pipelined score kernel: workgroups, LDS bytes
+  size_t lds_pipe = 0;
 };
 
 kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int model, int sk,

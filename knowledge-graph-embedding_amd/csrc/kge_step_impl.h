@@ -1801,9 +1801,25 @@ static inline void launch_rel_seg(const StepArgs& A, hipStream_t st) {
   hipLaunchKernelGGL(rel_seg_kernel<0>, grid, dim3(kRsThreads), 0, st, A);
 }
 
+#include "kge_score_pipe.h"
+
 // ------------------------------------------------------------ dispatch
 template <template <int, int, int> class Model, int VEC, int NC, int SK>
 static void launch_score(const StepArgs& A, const StepGeom& G, hipStream_t st) {
+  if constexpr (NC == 1 && pipe_ok<Model<VEC, NC, SK>>::v) {
+    if (A.pipe) {
+      const dim3 grid((unsigned)G.nWG_pipe), blk(kPipeThreads);
+      if (A.side_mode == KGE_SIDE_HT)
+        hipLaunchKernelGGL((score_pipe_kernel<Model, VEC, SK, KGE_SIDE_HT>), grid, blk, G.lds_pipe, st, A);
+#ifndef KGE_ONLY_ONE
+      else if (A.side_mode == KGE_SIDE_H)
+        hipLaunchKernelGGL((score_pipe_kernel<Model, VEC, SK, KGE_SIDE_H>), grid, blk, G.lds_pipe, st, A);
+      else
+        hipLaunchKernelGGL((score_pipe_kernel<Model, VEC, SK, KGE_SIDE_T>), grid, blk, G.lds_pipe, st, A);
+#endif
+      return;
+    }
+  }
 #ifdef KGE_ONLY_ONE
   hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK, KGE_SIDE_HT>), dim3(G.nWG), dim3(kStepThreads), G.lds_score,
                      st, A);

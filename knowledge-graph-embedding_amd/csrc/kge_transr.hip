@@ -732,7 +732,9 @@ static void launch_tr(const StepArgs& A, const StepGeom& G, const TrArgs& T, con
       default: hipLaunchKernelGGL((transr_kernel<SK, 16>), grid, blk, lds, st, A, T); break;
     }
   } else {
+#ifndef KGE_ONLY_ONE
     launch_transr2<SK>(A, T, st);
+#endif   // (single-instance tuning builds, tools/variants.py: no two-per-CU units linked)
   }
   if (ev) (void)hipEventRecord(ev[2], st);
   if (A.train) {
