@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define KGE_ABI_VERSION 6
+#define KGE_ABI_VERSION 7
 
 typedef enum kge_status {
   KGE_OK = 0,
@@ -181,14 +181,10 @@ enum {
    *       update pass (remote_rows_from, relation gradients to grad_out[1]). */
   KGE_FLAG_OWNER = 128,
   KGE_FLAG_OWNER_MERGE = 256,
-  KGE_FLAG_DEBUG_NO_REL_SEG = 512,  /* test hook: the owner merge's update pass sums the
+  KGE_FLAG_DEBUG_NO_REL_SEG = 512   /* test hook: the owner merge's update pass sums the
                                        relation rows in the update kernel (one wave per
                                        relation) instead of the per-relation segment pass
                                        (same sums up to their order) */
-  KGE_FLAG_SCORE_CLASSIC = 1024     /* test / A-B hook: the one-generation score kernel
-                                       (every positive's workgroup resident at once)
-                                       instead of the pipelined one (TransE, rows of
-                                       <= 256 floats); same values up to summation order */
 };
 
 typedef struct kge_table {
@@ -317,6 +313,16 @@ typedef struct kge_step_desc {
                                  expected owner_batch * K_eff, + 4096)          */
   float* owner_err;           /* OWNER: set to 2 when the owned negatives exceed the capacity
                                  (their keys are dropped: the caller voids the step; nullable) */
+  /* ABI 7: the step's overflow flags without host-side launches (nullable):
+   * OWNER_MERGE | PHASE_SCORE: owner_flags_in [2] (exchange flag, owner_err)
+   *   -> owner_flags_out [3] = (in[0], in[1], in[0] + in[1]), then in zeroed
+   *   for the next step (the caller all-reduces out: each slot counts the
+   *   ranks that raised it, the last is the abort word);
+   * OWNER | PHASE_UPDATE: owner_sticky [2] = max(owner_sticky, owner_flags_out[0..1])
+   *   (the all-reduced flags, read before the abort check). */
+  float* owner_flags_in;
+  float* owner_flags_out;
+  float* owner_sticky;
 } kge_step_desc;
 
 /*
@@ -520,11 +526,16 @@ typedef struct kge_exchange_desc {
   int32_t* req_cnt;           /* [world] out, zero-filled by the caller          */
   float* err_flag;            /* device [1]: set to 1 on an overflow / bad id (nullable) */
   int32_t* status;            /* KGE_ERANGE on an id out of range (nullable)     */
+  void* zero_next;            /* ABI 7: zero-filled by this call (nullable; e.g. the other half of
+                                 a double-buffered [htab | req_cnt] the NEXT call will use: no
+                                 fill launch between steps). Must not overlap this call's arrays */
+  int64_t zero_next_bytes;    /* multiple of 4                                   */
 } kge_exchange_desc;
 
 kge_status kge_exchange_plan(const kge_exchange_desc* d, void* stream);
 
-/* Owner side of the exchange, over requested ids [world, cap] (cnt [world]):
+/* Owner side of the exchange, over requested ids [world, cap] (cnt [world]),
+ * or (POS) over a batch of remapped triples:
  *  KGE_XROWS_GATHER  rows[s][q] = shard row (ids[s][q] div world), every block
  *                    (source < 0) or block `source`;
  *  KGE_XROWS_SGD     shard row += -lr * clip / max(sqrt(*norm2), clip) * rows[s][q]
@@ -532,9 +543,13 @@ kge_status kge_exchange_plan(const kge_exchange_desc* d, void* stream);
  *                    BaseModel.py:327-328); one call per source, in rank order,
  *                    so a row several ranks touched gets their sums in that order;
  *  KGE_XROWS_ACCUM   acc row += rows[s][q] for block `source` (Adam: the dense
- *                    gradient of the shard, kge_apply follows).
+ *                    gradient of the shard, kge_apply follows);
+ *  KGE_XROWS_POS     (ABI 7) rows[2i] = shard row ids[3i], rows[2i + 1] = shard
+ *                    row ids[3i + 2] for i < cap: the positives' h / t rows of a
+ *                    batch remapped by kge_exchange_plan (shard = the extended
+ *                    table; cnt, world, rank, source unused).
  * SGD / ACCUM do nothing when abort_flag is set and *abort_flag != 0. */
-enum { KGE_XROWS_GATHER = 0, KGE_XROWS_SGD = 1, KGE_XROWS_ACCUM = 2 };
+enum { KGE_XROWS_GATHER = 0, KGE_XROWS_SGD = 1, KGE_XROWS_ACCUM = 2, KGE_XROWS_POS = 3 };
 
 typedef struct kge_exchange_rows_desc {
   int32_t mode;               /* KGE_XROWS_*                                     */

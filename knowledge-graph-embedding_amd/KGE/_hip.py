@@ -11,7 +11,7 @@ import threading
 
 import torch
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 KGE_OK, KGE_EINVAL, KGE_ERANGE, KGE_EHIP, KGE_ENOMEM_WORKSPACE, KGE_EUNSUPPORTED, KGE_EWORKSPACE = range(7)
 
@@ -28,7 +28,6 @@ FLAG_PHASE_UPDATE = 64
 FLAG_OWNER = 128
 FLAG_OWNER_MERGE = 256
 FLAG_DEBUG_NO_REL_SEG = 512   # test hook: relation rows in the update kernel (compact launches)
-FLAG_SCORE_CLASSIC = 1024     # test / A-B hook: the one-generation score kernel, not the pipelined one
 RANK_TRANS, RANK_ROT, RANK_MUL, RANK_DOT = range(4)
 RANK_FLAG_LANE_PASS = 1
 RPROJ_NONE, RPROJ_HYPER, RPROJ_RANK1 = range(3)
@@ -84,6 +83,7 @@ class kge_step_desc(ctypes.Structure):
         ("owner_batch", ctypes.c_int64), ("owner_rows_from", ctypes.c_int64),
         ("owner_records", ctypes.c_void_p), ("owner_stats", ctypes.c_void_p), ("owner_stats_out", ctypes.c_void_p),
         ("owner_key_capacity", ctypes.c_int64), ("owner_err", ctypes.c_void_p),
+        ("owner_flags_in", ctypes.c_void_p), ("owner_flags_out", ctypes.c_void_p), ("owner_sticky", ctypes.c_void_p),
     ]
 
 
@@ -119,10 +119,11 @@ class kge_exchange_desc(ctypes.Structure):
                 ("loopback", ctypes.c_int32), ("_pad", ctypes.c_int32), ("local_rows", ctypes.c_int64),
                 ("cap", ctypes.c_int64), ("htab", ctypes.c_void_p), ("hslots", ctypes.c_int64),
                 ("pos_out", ctypes.c_void_p), ("neg_out", ctypes.c_void_p), ("req_ids", ctypes.c_void_p),
-                ("req_cnt", ctypes.c_void_p), ("err_flag", ctypes.c_void_p), ("status", ctypes.c_void_p)]
+                ("req_cnt", ctypes.c_void_p), ("err_flag", ctypes.c_void_p), ("status", ctypes.c_void_p),
+                ("zero_next", ctypes.c_void_p), ("zero_next_bytes", ctypes.c_int64)]
 
 
-XROWS_GATHER, XROWS_SGD, XROWS_ACCUM = range(3)
+XROWS_GATHER, XROWS_SGD, XROWS_ACCUM, XROWS_POS = range(4)
 
 
 class kge_exchange_rows_desc(ctypes.Structure):

@@ -270,7 +270,7 @@ class FusedStep:
             d.owner_rows_from = o.get("rows_from", 0)
             d.global_entities = o.get("global_entities", 0)
             d.owner_key_capacity = int(o.get("key_capacity", 0))
-            for f in ("records", "stats", "stats_out", "err"):
+            for f in ("records", "stats", "stats_out", "err", "flags_in", "flags_out", "sticky"):
                 if o.get(f) is not None:
                     setattr(d, "owner_" + f, o[f].data_ptr())
         d.loss_out = self.loss_out.data_ptr()

@@ -611,18 +611,24 @@ class ShardedStep:
         self._own = None   # (its buffers point into the old table)
         if hasattr(self, "_sf"):
             self._sf = None
-        # the plan's per-step zero state (hash table, per-owner counts, error
-        # flag) in one buffer: one fill per step instead of three launches
+        # the plan's per-step zero state: two [hash table | per-owner counts]
+        # halves, used by alternate steps (owner mode: each step's plan zeroes
+        # the half the previous step used, kge_exchange_desc.zero_next -- no
+        # fill launch), then the error flags (zeroed by the owner merge after
+        # it reads them; sparse mode fills the whole buffer once per step)
         zb = -(-(G * 4) // 8) * 8
-        zero = torch.zeros(hs * 8 + zb + 8, dtype=torch.uint8, device=dev)
+        half = hs * 8 + zb
+        zero = torch.zeros(2 * half + 8, dtype=torch.uint8, device=dev)
+        halves = [zero[k * half:(k + 1) * half] for k in range(2)]
         b = {"n_occ": n_occ, "dtype": idx_dtype, "cap": cap, "ext": ext, "hslots": hs, "pos_rows": pos_rows,
-             "pos_base": self.Es + G * cap, "zero": zero,
-             "htab": zero[:hs * 8].view(torch.int64),
-             "req_cnt": zero[hs * 8:hs * 8 + G * 4].view(torch.int32),
+             "pos_base": self.Es + G * cap, "zero": zero, "halves": halves, "parity": 0,
+             "htabs": [h[:hs * 8].view(torch.int64) for h in halves],
+             "req_cnts": [h[hs * 8:hs * 8 + G * 4].view(torch.int32) for h in halves],
              "req_ids": torch.zeros(G * cap, dtype=idx_dtype, device=dev),
-             "err": zero[hs * 8 + zb:hs * 8 + zb + 4].view(torch.float32),
-             # [exchange plan's flag | owner pass's flag], zeroed with the rest
-             "errs": zero[hs * 8 + zb:hs * 8 + zb + 8].view(torch.float32)}
+             "err": zero[2 * half:2 * half + 4].view(torch.float32),
+             # [exchange plan's flag | owner pass's flag]
+             "errs": zero[2 * half:2 * half + 8].view(torch.float32)}
+        b["htab"], b["req_cnt"] = b["htabs"][0], b["req_cnts"][0]
         if self.multi:
             b["recv_cnt"] = torch.zeros(G, dtype=torch.int32, device=dev)
             b["recv_ids"] = torch.zeros(G * cap, dtype=idx_dtype, device=dev)
@@ -632,16 +638,28 @@ class ShardedStep:
         self._ext = b
         return b
 
-    def _xrows(self, b, mode, rows, rows_ld, view, source=-1, norm2_ptr=None, lr=0.0, acc=None):
-        """kge_exchange_rows on this rank's owned rows ``view`` (a column view of the shard)."""
+    def _flip(self, b):
+        """Owner mode: this step's [hash table | counts] half (zeroed by the
+        previous step's plan, or never used) and the half to zero now."""
+        p = b["parity"] = 1 - b["parity"]
+        b["htab"], b["req_cnt"] = b["htabs"][p], b["req_cnts"][p]
+        if not self.multi:
+            b["recv_cnt"] = b["req_cnt"]
+        return b["halves"][1 - p]
+
+    def _xrows(self, b, mode, rows, rows_ld, view, source=-1, norm2_ptr=None, lr=0.0, acc=None, ids=None,
+               count=None):
+        """kge_exchange_rows on this rank's owned rows ``view`` (a column view of
+        the shard); POS mode: ``count`` triples ``ids`` (extended-table rows)
+        -> their h, t rows of ``view`` into ``rows``."""
         d = _hip.kge_exchange_rows_desc()
         d.mode = mode
         d.idx_dtype = _hip.IDX_I64 if b["dtype"] == torch.int64 else _hip.IDX_I32
         d.shard = _hip.table(view)
-        d.ids = b["recv_ids"].data_ptr()
+        d.ids = (ids if ids is not None else b["recv_ids"]).data_ptr()
         d.cnt = b["recv_cnt"].data_ptr()
         d.world, d.rank, d.source = self.G, self.g, source
-        d.cap = b["cap"]
+        d.cap = b["cap"] if count is None else count
         d.rows = rows.data_ptr()
         d.rows_ld = rows_ld
         d.acc = acc.data_ptr() if acc is not None else None
@@ -823,14 +841,17 @@ class ShardedStep:
              "stats": torch.zeros(G * Bn, 4, dtype=torch.float32, device=dev),
              "lpos": torch.zeros(Bn, 3, dtype=idx_dtype, device=dev),   # the batch in extended-table rows
              "runs": {},
-             "err": b["errs"][1:]}   # (zeroed per step by b["zero"])
+             "err": b["errs"][1:]}   # (zeroed each step by the merge, after it reads it)
         fo.plane_fn = lambda ns, n: o["base_plane"]   # rank 0's planes of this step (set per step)
         common = {"world": G, "rank": g, "batch": Bn}
         # key positions for the owned negatives: ~Bn Keff expected (1/G of the
         # G Bn virtual positives' slots), more when ownership is skewed
         o["key_cap"] = min(G * Bn * Keff, int(math.ceil(max(1.25, self.slack) * Bn * Keff)) + max(4096, self.cap_floor))
+        small = self.red[-8:]
+        # (flags_out / sticky: the owner update pass folds the all-reduced flags
+        # into the sticky max -- no launch of its own)
         fo.owner = dict(common, rows_from=b["pos_base"], global_entities=self.E, err=o["err"], stats=o["stats"],
-                        key_capacity=o["key_cap"])
+                        key_capacity=o["key_cap"], flags_out=small[5:8], sticky=self.xerr)
         fo.flags = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER | _hip.FLAG_PHASE_SCORE
         # the record width of this plan, then the record buffers
         probe = fo.describe(o["gtrip"], True, _opt.SGD(0.01), neg_ids=o["gneg"])
@@ -843,7 +864,10 @@ class ShardedStep:
         o["rec_in"] = torch.zeros(G * Bn, R, dtype=torch.float32, device=dev) if self.multi else o["rec"]
         o["stats_mine"] = o["stats"][g * Bn:(g + 1) * Bn]
         fo.owner["records"] = o["rec"]
-        fm.owner = dict(common, records=o["rec_in"], stats_out=o["stats_mine"])
+        # (flags_in -> flags_out: the merge hands the step's flags to the
+        # all-reduce buffer and zeroes them)
+        fm.owner = dict(common, records=o["rec_in"], stats_out=o["stats_mine"], flags_in=b["errs"],
+                        flags_out=small[5:8])
         self._own = o
         return b, o
 
@@ -898,7 +922,9 @@ class ShardedStep:
         st = _hip.stream_handle(self.device)
         loop = self.loopback
         # 1. the positives' rows: plan (no negatives), requests, owners gather, rows back
-        b["zero"].zero_()   # htab | req_cnt | err
+        # (this step's hash table / counts were zeroed by the previous step's
+        # plan, which zeroes the other half now; the flags by the last merge)
+        zero_next = self._flip(b)
         lpos = o["lpos"]
         x = o.get("x")
         if x is None:   # (built once per plan: only the batch address changes per step)
@@ -910,13 +936,15 @@ class ShardedStep:
             x.world, x.rank, x.loopback = G, g, int(loop)
             x.local_rows = self.Es
             x.cap = cap
-            x.htab, x.hslots = b["htab"].data_ptr(), b["hslots"]
+            x.hslots = b["hslots"]
             x.pos_out, x.neg_out = lpos.data_ptr(), lpos.data_ptr()
-            x.req_ids, x.req_cnt = b["req_ids"].data_ptr(), b["req_cnt"].data_ptr()
+            x.req_ids = b["req_ids"].data_ptr()
             x.err_flag = b["err"].data_ptr()
             x.status = self.status.data_ptr()
             o["x"] = x
         x.pos = x.neg = batch.data_ptr()
+        x.htab, x.req_cnt = b["htab"].data_ptr(), b["req_cnt"].data_ptr()
+        x.zero_next, x.zero_next_bytes = zero_next.data_ptr(), zero_next.numel()
         _hip.check(self.lib.kge_exchange_plan(ctypes.byref(x), st), "kge_exchange_plan")
         blocks = ext[self.Es:b["pos_base"]]
         if self.multi:
@@ -929,8 +957,9 @@ class ShardedStep:
         # 2. every rank's positives: rows (h, t of positive v at pos_base + 2v, + 1) and triples
         P = ext[b["pos_base"]:b["pos_base"] + 2 * G * Bn]
         mine = P[2 * g * Bn:2 * (g + 1) * Bn]
-        # (gathered straight into P: the source rows [0, pos_base) and P do not overlap)
-        torch.index_select(ext[:b["pos_base"]], 0, lpos[:, 0::2].reshape(-1).to(torch.int64), out=mine)
+        # (gathered straight into P by kge_exchange_rows' POS mode: the source
+        # rows [0, pos_base) and P do not overlap)
+        self._xrows(b, _hip.XROWS_POS, mine, C, ext[:b["pos_base"]], ids=lpos, count=Bn)
         gtrip = o["gtrip"]
         if self.multi:   # (one rank: P is `mine`, the virtual batch is the batch)
             ex.all_gather(P, mine)
@@ -969,14 +998,13 @@ class ShardedStep:
         else:
             fm.flags, fm.abort = f_ms, None
             fm(lpos, is_train, opt)
-        # 6. [norm^2 x4 | loss | exchange flag | owner flag | any flag], the stats
-        small[5:7].copy_(b["errs"])
-        torch.sum(b["errs"], dim=0, keepdim=True, out=small[7:8])
+        # 6. [norm^2 x4 | loss | exchange flag | owner flag | any flag] (the
+        # merge wrote the flags and zeroed them for the next step), the stats
         if self.multi:
             ex.all_reduce(small)
             ex.all_gather(o["stats"], o["stats_mine"])
-        torch.maximum(self.xerr, small[5:7], out=self.xerr)
-        if not is_train:
+        if not is_train:   # (training steps: the owner update pass keeps the sticky max)
+            torch.maximum(self.xerr, small[5:7], out=self.xerr)
             return self.loss
         # 7. the owned negatives' rows, then 8. the positives' rows
         f_ou = _hip.FLAG_NO_TABLE_CONSTRAINT | _hip.FLAG_OWNER | _hip.FLAG_PHASE_UPDATE

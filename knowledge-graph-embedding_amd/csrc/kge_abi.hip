@@ -39,18 +39,6 @@ inline bool aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
 
 constexpr int kWaves = 4;      // constrain / sample / apply kernels: waves per workgroup
 
-// compute units of the current device (the pipelined score kernel's grid:
-// one workgroup per CU); 256 (MI355X) when no device answers
-int device_cus() {
-  static int cached[16] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
-  if (dev < 16 && cached[dev] > 0) return cached[dev];
-  int n = 0;
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-  if (dev < 16) cached[dev] = n;
-  return n;
-}
 
 struct Plan {
   StepArgs A;
@@ -331,31 +319,6 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   if (P.G.lds_score > 160 * 1024)
     return fail(KGE_EUNSUPPORTED, "LDS budget exceeded (score kernel %zu bytes)", P.G.lds_score);
   P.sk = score_sk(d->score_kind, p);
-  // the pipelined score kernel (kge_score_pipe.h): TransE rows of one
-  // fragment chunk; a run of ppw positives per 16-wave workgroup, one
-  // workgroup per CU, every wave a share of every positive's slots
-  {
-    const int NI = P.sk == SK_DOT ? 3 : 2;   // accumulator images per wave (rec_img<TransE>)
-    int swp = (int)ceil_div(Keff, kPipeWaves);
-    if (d->corrupt_side == KGE_SIDE_HT) swp = (int)round_up(swp, 2);
-#ifdef KGE_NO_PIPE
-    const bool pipe = false;   // (A-B builds: tools/variants.py)
-#else
-    const bool pipe = model == KGE_MODEL_TRANSE && ncp == 1 && !own && !omerge &&
-                      !(d->flags & KGE_FLAG_SCORE_CLASSIC) && swp <= kPipeMaxSW;
-#endif
-    if (pipe) {
-      const int64_t ppw = ceil_div(B, device_cus());
-      const size_t lds = (size_t)pipe_lds((int)entc, NI, Keff, (int)ppw).total;
-      if (lds <= 160 * 1024) {
-        A.pipe = true;
-        A.pipe_ppw = (int32_t)ppw;
-        A.pipe_sw = swp;
-        P.G.nWG_pipe = (int)ceil_div(B, ppw);
-        P.G.lds_pipe = lds;
-      }
-    }
-  }
 
   A.ent = TabView{d->ent.data, d->ent.ld, (int32_t)entc, E};
   A.n_ent = d->shard_count > 1 ? d->global_entities : E;
@@ -473,6 +436,9 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
     A.own_stats_out = d->owner_stats_out;
     A.own_cap = (uint32_t)(own ? T : 0);
     A.own_err = d->owner_err;
+    A.own_flags_in = d->owner_flags_in;
+    A.own_flags_out = d->owner_flags_out;
+    A.own_sticky = d->owner_sticky;
     A.own_keys = own;
     A.n_ent = own ? d->global_entities : E;   // (merge: ids are the caller's table rows)
   }
@@ -487,8 +453,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
   P.o_coef = take((uint64_t)(B << kshift) * 8);   // indexed by destination code
   P.o_snap = take((uint64_t)B * nsnap * entc * 4);
   P.o_gpos = take((uint64_t)(own ? 1 : B * 3 * rowlen) * 4);   // (the owner pass keeps no positive gradients)
-  P.o_part = take((uint64_t)std::max<int64_t>((transr || proj) ? std::max<int64_t>(nWG, B) : nWG, P.G.nWG_pipe) * 8 *
-                  4);   // one partial per positive (TransR / projection) or per score workgroup
+  P.o_part = take((uint64_t)((transr || proj) ? std::max<int64_t>(nWG, B) : nWG) * 8 * 4);   // one partial per positive
   P.o_list = take((uint64_t)nlists * cap * 4);
   P.o_ovf = take((uint64_t)T * 8);
   P.o_upart = take((uint64_t)P.G.gridU * 2 * 4);   // gradient norm^2 | entity norm^2 (dense mode)
@@ -559,8 +524,7 @@ kge_status make_plan(const kge_step_desc* d, Plan* pl) {
                          (int64_t)P.o_upart, (int64_t)P.o_leaders, (int64_t)P.o_sorted, (int64_t)P.o_relseg,
                          (int64_t)P.o_gneg, (int64_t)P.o_dpart, (int64_t)P.o_owncodes, (int64_t)P.o_segraw, (int64_t)P.o_segkeys,
                          (int64_t)P.o_segpart, T,
-                         (int64_t)d->owner_world, (int64_t)d->owner_batch, (int64_t)A.pipe, A.pipe_ppw, A.pipe_sw,
-                         P.G.nWG_pipe};
+                         (int64_t)d->owner_world, (int64_t)d->owner_batch};
     uint32_t h = 2166136261u;
     for (const int64_t v : f)
       for (int b = 0; b < 8; ++b) h = (h ^ (uint32_t)((uint64_t)v >> (8 * b) & 0xFF)) * 16777619u;

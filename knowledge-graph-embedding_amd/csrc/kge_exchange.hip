@@ -42,6 +42,13 @@ constexpr int kAggOwners = 64;
 __global__ __launch_bounds__(256) void exch_insert_kernel(kge_exchange_desc d, int64_t n) {
   __shared__ int s_cnt[kAggOwners];
   __shared__ int s_base[kAggOwners];
+  // the next call's zero state (zero_next), grid-stride
+  if (d.zero_next) {
+    uint32_t* z = reinterpret_cast<uint32_t*>(d.zero_next);
+    const int64_t nw = d.zero_next_bytes / 4;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += (int64_t)gridDim.x * blockDim.x)
+      z[q] = 0u;
+  }
   const bool i64 = d.idx_dtype == KGE_IDX_I64;
   const uint64_t mask = (uint64_t)d.hslots - 1;
   const bool agg = d.world <= kAggOwners;
@@ -131,6 +138,30 @@ __global__ __launch_bounds__(256) void exch_remap_kernel(kge_exchange_desc d, in
   if (over && d.err_flag) d.err_flag[0] = 1.f;
 }
 
+// POS mode: one wave per (positive, h / t), the row copied float4-wide when the strides allow
+__global__ __launch_bounds__(256) void exch_pos_rows_kernel(kge_exchange_rows_desc d) {
+  const bool i64 = d.idx_dtype == KGE_IDX_I64;
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x / KGE_WAVE) + wave_id();
+  if (w >= 2 * d.cap) return;
+  const int64_t i = w >> 1;
+  const int64_t r = load_idx(d.ids, 3 * i + 2 * (w & 1), i64);
+  if (r < 0 || r >= d.shard.rows) {
+    if (lane_id() == 0) set_status(d.status, KGE_ERANGE);
+    return;
+  }
+  const float* src = d.shard.data + r * d.shard.ld;
+  float* dst = d.rows + w * d.rows_ld;
+  const int cols = (int)d.shard.cols;
+  const bool v4 = cols % 4 == 0 && d.shard.ld % 4 == 0 && d.rows_ld % 4 == 0 &&
+                  ((uintptr_t)d.shard.data % 16) == 0 && ((uintptr_t)d.rows % 16) == 0;
+  if (v4) {
+    for (int c = 4 * lane_id(); c < cols; c += 4 * KGE_WAVE)
+      *reinterpret_cast<float4*>(dst + c) = *reinterpret_cast<const float4*>(src + c);
+  } else {
+    for (int c = lane_id(); c < cols; c += KGE_WAVE) dst[c] = src[c];
+  }
+}
+
 // owner side: one wave per (block, position); float4 rows when the strides allow
 __global__ __launch_bounds__(256) void exch_rows_kernel(kge_exchange_rows_desc d, int32_t b0, int32_t nb) {
   if ((d.mode == KGE_XROWS_SGD || d.mode == KGE_XROWS_ACCUM) && d.abort_flag && *d.abort_flag != 0.f) return;
@@ -202,7 +233,15 @@ kge_status kge_exchange_plan(const kge_exchange_desc* d, void* stream) {
   if (d->batch < 0 || d->n_neg < 0 || d->cap <= 0 || d->local_rows < 0) return xfail("kge_exchange_plan: bad sizes");
   if (d->n_entities <= 0 || d->n_entities > (int64_t)0xFFFFFFFE) return xfail("kge_exchange_plan: n_entities out of range");
   const int64_t n = 2 * d->batch + d->n_neg;
-  if (n == 0) return KGE_OK;
+  if (d->zero_next && (d->zero_next_bytes < 0 || d->zero_next_bytes % 4 != 0 || ((uintptr_t)d->zero_next % 4) != 0))
+    return xfail("kge_exchange_plan: zero_next must be 4-byte aligned, a multiple of 4 bytes");
+  if (n == 0) {
+    if (d->zero_next && d->zero_next_bytes > 0) {
+      const hipError_t e = hipMemsetAsync(d->zero_next, 0, (size_t)d->zero_next_bytes, (hipStream_t)stream);
+      if (e != hipSuccess) { kge_set_error(hipGetErrorString(e)); return KGE_EHIP; }
+    }
+    return KGE_OK;
+  }
   if (d->hslots < 2 * n || (d->hslots & (d->hslots - 1)) != 0)
     return xfail("kge_exchange_plan: hslots must be a power of two >= 2 x occurrences");
   if (!d->pos || (d->n_neg && !d->neg) || !d->pos_out || (d->n_neg && !d->neg_out) || !d->htab || !d->req_ids ||
@@ -222,8 +261,24 @@ kge_status kge_exchange_plan(const kge_exchange_desc* d, void* stream) {
 
 kge_status kge_exchange_rows(const kge_exchange_rows_desc* d, void* stream) {
   if (!d) return xfail("null descriptor");
-  if (d->mode != KGE_XROWS_GATHER && d->mode != KGE_XROWS_SGD && d->mode != KGE_XROWS_ACCUM)
+  if (d->mode != KGE_XROWS_GATHER && d->mode != KGE_XROWS_SGD && d->mode != KGE_XROWS_ACCUM &&
+      d->mode != KGE_XROWS_POS)
     return xfail("kge_exchange_rows: bad mode");
+  if (d->mode == KGE_XROWS_POS) {
+    if (d->idx_dtype != KGE_IDX_I32 && d->idx_dtype != KGE_IDX_I64) return xfail("kge_exchange_rows: bad idx_dtype");
+    if (d->cap < 0 || !d->ids || !d->rows || !d->shard.data || d->shard.cols <= 0 || d->shard.ld < d->shard.cols ||
+        d->rows_ld < d->shard.cols)
+      return xfail("kge_exchange_rows: POS needs ids, rows, a shard and rows_ld >= its columns");
+    if (d->cap == 0) return KGE_OK;
+    const unsigned blocks = (unsigned)((2 * d->cap + 3) / 4);
+    hipLaunchKernelGGL(exch_pos_rows_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *d);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+      kge_set_error(hipGetErrorString(e));
+      return KGE_EHIP;
+    }
+    return KGE_OK;
+  }
   if (d->idx_dtype != KGE_IDX_I32 && d->idx_dtype != KGE_IDX_I64) return xfail("kge_exchange_rows: bad idx_dtype");
   if (d->world < 1 || d->rank < 0 || d->rank >= d->world || d->cap <= 0) return xfail("kge_exchange_rows: bad sizes");
   if (!d->shard.data || d->shard.cols <= 0 || d->shard.ld < d->shard.cols || d->rows_ld < d->shard.cols)

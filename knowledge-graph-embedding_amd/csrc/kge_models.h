@@ -236,7 +236,6 @@ struct TransE {
   static constexpr bool CPLX = false;
   static constexpr bool WIDE = false;   // score kernel fits 128 VGPRs at one chunk (4 waves / SIMD)
   static constexpr bool SELF_CTX = false;   // context rows computed by the score kernel itself (RESCAL)
-  static constexpr bool PIPE = NC == 1;     // the pipelined score kernel (kge_score_pipe.h) covers it
   // owner-side scoring records carry the h and t accumulators only: an Lp
   // score is a function of h + r - t, so d/dr = d/dh for a t-corrupt slot and
   // -d/dt for an h-corrupt one -- the r accumulator is h - t (finish below);
@@ -254,9 +253,9 @@ struct TransE {
     load_ctx_raw(c, ent, rel, h, r, t);
     ctx_finish(c, mp);
   }
-  // load_ctx in two halves (the pipelined score kernel issues the next
-  // positive's rows, then finishes them after the current tail): the raw
-  // rows (h parked in X), then the normalisation and the combined rows
+  // load_ctx in two halves (the score kernel issues the context rows with
+  // its first row batch and finishes them after): the raw rows (h parked
+  // in X), then the normalisation and the combined rows
   __device__ static void load_ctx_raw(Ctx& c, const TabView& ent, const TabView& rel, int64_t h, int64_t r,
                                       int64_t t) {
     load_row(c.X, ent.row(h), ent.cols);

@@ -240,6 +240,13 @@ __global__ __launch_bounds__(kMergeWaves * KGE_WAVE) void owner_merge_kernel(Ste
       A.ctl->ovf_len = __hip_atomic_exchange(&A.ctl->ovf_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       A.ctl->lng_count = 0u;   // the update pass's deferred long destinations
       A.ctl->score_pending = A.sig;   // (the merge is always a PHASE_SCORE call: the phase gate's token)
+      if (A.own_flags_out) {   // the step's flags for the caller's all-reduce, zeroed for the next step
+        const float x = A.own_flags_in ? A.own_flags_in[0] : 0.f, o = A.own_flags_in ? A.own_flags_in[1] : 0.f;
+        A.own_flags_out[0] = x;
+        A.own_flags_out[1] = o;
+        A.own_flags_out[2] = x + o;
+        if (A.own_flags_in) { A.own_flags_in[0] = 0.f; A.own_flags_in[1] = 0.f; }
+      }
     }
   }
 }
@@ -271,7 +278,13 @@ __device__ __forceinline__ void phase_gate_check(StepCtl* ctl, uint32_t sig, int
 // refuses the poisoned workspace.
 template <int SK>
 __global__ __launch_bounds__(256) void owner_coef_kernel(StepArgs A) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) phase_gate_check(A.ctl, A.sig, A.status);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    phase_gate_check(A.ctl, A.sig, A.status);
+    if (A.own_sticky && A.own_flags_out) {   // (every training step, aborted ones included)
+      A.own_sticky[0] = fmaxf(A.own_sticky[0], A.own_flags_out[0]);
+      A.own_sticky[1] = fmaxf(A.own_sticky[1], A.own_flags_out[1]);
+    }
+  }
   if (ws_refused(A.ctl, A.sig, A.status, nullptr)) return;
   if (A.abort_flag && *A.abort_flag != 0.f) return;
   const uint32_t n = min(A.ctl->own_len, A.own_cap);

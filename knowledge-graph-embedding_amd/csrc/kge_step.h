@@ -219,10 +219,6 @@ struct StepArgs {
   int32_t nP;       // positives per score workgroup = kStepWaves / wpp
   int32_t SW;       // negative slots per wave
   int32_t nWG;      // score workgroups
-  // pipelined score kernel (kge_score_pipe.h): a run of pipe_ppw positives
-  // per 16-wave workgroup, pipe_sw negative slots per wave per positive
-  bool pipe = false;
-  int32_t pipe_ppw = 0, pipe_sw = 0;
   int32_t cap;      // destination list capacity (entries per destination)
   int32_t snap_cols, gcols, rel_gcols;
   uint32_t nkeyneg; // B << kshift: codes below are negatives (i << kshift | j), above positive rows (+4i+c)
@@ -274,6 +270,9 @@ struct StepArgs {
   uint32_t* own_codes = nullptr;    // owner: [own_cap] destination code per key position (~0: padding)
   uint32_t own_cap = 0;             // owner: key positions available (grid of the update launch)
   float* own_err = nullptr;         // owner: set to 2 when the owned keys exceed own_cap
+  float* own_flags_in = nullptr;    // merge: the step's [exchange, owner] flags (read, then zeroed)
+  float* own_flags_out = nullptr;   // merge: out [3]; owner update: the all-reduced copy (read)
+  float* own_sticky = nullptr;      // owner update: [2] running max of the all-reduced flags
   bool own_keys = false;            // update kernel: compact key positions [0, ctl->own_len)
 };
 // accumulator images per owner record: M::REC_IMG when the model declares it
@@ -286,8 +285,6 @@ struct StepGeom {
   int vec, nc;
   int nWG, gridU;
   size_t lds_score;
-  int nWG_pipe = 0;        // pipelined score kernel: workgroups, LDS bytes
-  size_t lds_pipe = 0;
 };
 
 kge_status launch_step_elementwise(const StepArgs& A, const StepGeom& G, int model, int sk,

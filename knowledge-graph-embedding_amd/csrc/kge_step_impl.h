@@ -49,9 +49,17 @@
 #define KGE_GUARD_KU 1      // update kernel: workspace plan guard at entry (tuning / A-B knob)
 #endif
 #ifndef KGE_FILE_EARLY
-#define KGE_FILE_EARLY 0    // score kernel: negatives' keys filed during the stream (1: claims after the first
-                            // batch's loads, stored after its compute; 2: claims after the stream, stored after
-                            // the merge barrier; 0: in the finalise pass) (A-B knob)
+// score kernel: when the negatives' keys are filed. 2 (default): each lane's
+// slot claims its destination (counter add / hash-slot CAS) right after the
+// row stream and stores the code after the merge barrier, so the claim's
+// round trip hides under the barrier wait and the merge (C2 KS 53.7 -> 48.7
+// us, profiles/r06e); 1: claims after the first batch's loads (slower: 55.4);
+// 0: claim and store in the finalise pass (A-B knob)
+#define KGE_FILE_EARLY 2
+#endif
+#ifndef KGE_CTX_LATE
+#define KGE_CTX_LATE 1      // score kernel: the positive's context rows finished after the first row batch's
+                            // loads are issued (one dependent round trip fewer per wave) (A-B knob)
 #endif
 #ifndef KGE_UPDATE_U
 #define KGE_UPDATE_U 8      // update kernel: list entries in flight per wave at NC = 1 (tuning knob)
@@ -144,37 +152,46 @@ __device__ __forceinline__ float neg_coef(const StepArgs& A, float s, float sp, 
 // skewed entities -- which then start early instead of forming the update
 // launch's tail), then the negatives'
 struct KeyClaim {
-  uint32_t r;   // list position the key took
-  uint32_t h;   // compact launches: its hash slot
+  uint32_t r;               // list position the key took (compact: resolved by bin_commit)
+  uint32_t h;               // compact launches: its hash slot
+  unsigned long long cur;   // compact launches: what the first CAS found
 };
-// the returning half of bin_key: the destination's counter (or hash slot)
-// taken. Non-compact: one atomic whose result is only needed by bin_commit,
-// so the two can be issued apart (the score kernel's early filing)
+// The returning half of bin_key, issued: the destination's counter (one
+// atomic add) or, compact launches, the first compare-and-swap on the
+// destination's hash slot. Nothing here waits for the result, so the
+// score kernel can issue its keys' claims and go on (early filing):
+// bin_commit uses the results.
 __device__ __forceinline__ KeyClaim bin_claim(const StepArgs& A, int64_t dest) {
   KeyClaim c;
   if (A.compact) {
     const unsigned long long key = (unsigned long long)((uint32_t)dest + 1u) << 32;
-    uint32_t h = ((uint32_t)dest * 2654435761u) >> A.hshift;
-    for (;;) {   // at most one pass: the table has >= 2x as many slots as keys
-      const unsigned long long cur = atomicCAS(&A.htab[h], 0ull, key | 1ull);
-      if (cur == 0ull) { c.r = 0u; break; }
-      if ((cur & 0xFFFFFFFF00000000ull) == key) { c.r = (uint32_t)atomicAdd(&A.htab[h], 1ull); break; }
-      h = (h + 1u) & A.hmask;
-    }
-    c.h = h;
+    c.h = ((uint32_t)dest * 2654435761u) >> A.hshift;
+    c.cur = atomicCAS(&A.htab[c.h], 0ull, key | 1ull);
+    c.r = 0u;
   } else {
     c.r = atomicAdd(&A.cnt[dest], 1u);
     c.h = 0u;
+    c.cur = 0ull;
   }
   return c;
 }
-// the storing half: the code into the destination's list at the claimed
-// position (the overflow list past capacity); compact launches also record
-// the key's leader-table entry
+// The storing half: compact launches first finish the claim (an empty slot
+// taken -- the common case on a large table -- or one atomic add on the
+// slot that holds the destination, else probe on: the table has >= 2x as
+// many slots as keys), then the code goes into the destination's list at
+// the claimed position (the overflow list past capacity) and compact
+// launches record the key's leader-table entry
 __device__ __forceinline__ void bin_commit(const StepArgs& A, int64_t dest, uint32_t code, KeyClaim c,
                                            uint32_t kpos_own = ~0u) {
   int64_t li = dest;   // list index
   if (A.compact) {
+    const unsigned long long key = (unsigned long long)((uint32_t)dest + 1u) << 32;
+    for (;;) {
+      if (c.cur == 0ull) { c.r = 0u; break; }
+      if ((c.cur & 0xFFFFFFFF00000000ull) == key) { c.r = (uint32_t)atomicAdd(&A.htab[c.h], 1ull); break; }
+      c.h = (c.h + 1u) & A.hmask;
+      c.cur = atomicCAS(&A.htab[c.h], 0ull, key | 1ull);
+    }
     li = c.h;
     // (the owner pass hands each key its position in the workgroup's block)
     const uint32_t kpos = kpos_own != ~0u ? kpos_own
@@ -256,6 +273,11 @@ template <int N, class Fn>
 __device__ __forceinline__ void static_for(Fn&& fn) {
   static_for_impl(fn, std::make_integer_sequence<int, N>{});
 }
+
+// models whose context load comes in two halves (load_ctx_raw, ctx_finish)
+template <class M, class = void> struct ctx_split { static constexpr bool v = false; };
+template <class M>
+struct ctx_split<M, std::void_t<decltype(&M::ctx_finish)>> { static constexpr bool v = true; };
 
 // corruption kind of row u of a stream batch (batches start on an even slot:
 // 'h+t' slots alternate h-corrupt / t-corrupt, BaseModel.py:353-356)
@@ -460,6 +482,19 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   }
   KGE_PROF(0);
 
+  // early filing (KGE_FILE_EARLY): this lane's slot jbeg + lane, its claim
+  const bool early = KGE_FILE_EARLY != 0 && !OWN && A.train && A.SW <= KGE_WAVE;
+  const int jfile = jbeg + lane;
+  int64_t kdest = 0;
+  KeyClaim kc{0u, 0u};
+  auto claim_early = [&]() {
+    __builtin_amdgcn_sched_barrier(0);   // (after the batch's row loads, not before them)
+    if (jfile < jend) { kdest = ids[jfile]; kc = bin_claim(A, kdest); }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto commit_early = [&]() {
+    if (jfile < jend) bin_commit(A, kdest, ((uint32_t)i << A.kshift) | (uint32_t)jfile, kc);
+  };
   typename M::Ctx ctx;
   float Mrun = -INFINITY, Zs = 0.f, csum = 0.f;
   float nrm[4] = {0.f, 0.f, 0.f, 0.f};
@@ -507,19 +542,31 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
       }
     }
     __syncthreads();   // `red` is reused for the wave states below
-  } else if (active) {
-    M::load_ctx(ctx, A.ent, A.rel, ph, pr, pt, mp);
   }
-  if (active) {
-    {   // the positive's score, in every wave (hinge / logistic weights need it)
-      F a, b, E0;
-      E0.zero();
-      M::fwd(ctx, KIND_POS, E0, a, b);
-      const float part = score_partial<SK, M::CPLX>(a, b, A.p);
-      Rp = lane_reduce<5, SK == SK_PINF>(part);
-      if (SK == SK_PINF) tp = lane_reduce<5, false>(tie_partial<M::CPLX>(a, Rp));
-      sp = score_value<SK>(Rp, A.pw, &lpp, A.p);
+  // KGE_CTX_LATE: the context rows' loads go out now, their combination (and
+  // the positive's score) after the first row batch's loads are issued
+  constexpr bool LATE = KGE_CTX_LATE && !OWN && ctx_split<M>::v;
+  bool ctx_done = !LATE;
+  if constexpr (!M::SELF_CTX) {
+    if (active) {
+      if constexpr (LATE) M::load_ctx_raw(ctx, A.ent, A.rel, ph, pr, pt);
+      else M::load_ctx(ctx, A.ent, A.rel, ph, pr, pt, mp);
     }
+  }
+  // the positive's score, in every wave (hinge / logistic weights need it)
+  auto pos_score = [&]() {
+    if constexpr (LATE) M::ctx_finish(ctx, mp);
+    F a, b, E0;
+    E0.zero();
+    M::fwd(ctx, KIND_POS, E0, a, b);
+    const float part = score_partial<SK, M::CPLX>(a, b, A.p);
+    Rp = lane_reduce<5, SK == SK_PINF>(part);
+    if (SK == SK_PINF) tp = lane_reduce<5, false>(tie_partial<M::CPLX>(a, Rp));
+    sp = score_value<SK>(Rp, A.pw, &lpp, A.p);
+    ctx_done = true;
+  };
+  if (active) {
+    if (!LATE) pos_score();
     const int lrow = lane >> SH;
     const bool lead = (lane & (LPR - 1)) == 0;
     // RAW: unmasked row loads, only the score partial masked (NRM_FROM_R
@@ -565,6 +612,12 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
         if (j0 + ROWS < se) issue(En, j0 + ROWS, sb, se);
       } else {
         issue(E, j0, sb, se);
+      }
+      if constexpr (KGE_FILE_EARLY == 1 && !OWN) {
+        if (early && j0 == sb) claim_early();
+      }
+      if constexpr (LATE) {
+        if (!ctx_done) pos_score();
       }
       if (A.fuse_norm) {
         // fused _constraint_loss: each sampled row normalised in registers
@@ -657,6 +710,9 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
         const float Mu = SK == SK_PINF ? bcast(Rl, u << SH) : SK == SK_PGEN ? A.p : 0.f;
         M::template bwdk<kind_at<S2>(u)>(ctx, E[u], a[u], b[u], alu, Mu, accH, accR, accT, nrm, mp);
       });
+      if constexpr (KGE_FILE_EARLY == 1 && !OWN) {
+        if (early && j0 == sb) commit_early();
+      }
     }
     };
     auto stream_lk = [&](auto sidec, const int sb, const int se) {
@@ -668,6 +724,12 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
       if constexpr (SIDE == KGE_SIDE_HT) stream_lk(std::integral_constant<int, KGE_SIDE_T>{}, tb, te);
     } else {
       stream_lk(std::integral_constant<int, SIDE>{}, jbeg, jend);
+      if constexpr (LATE) {
+        if (!ctx_done) pos_score();   // (a wave with no slots)
+      }
+      if constexpr (KGE_FILE_EARLY == 2) {
+        if (early) claim_early();
+      }
     }
     M::finish(accH, accR, accT);
   }
@@ -739,6 +801,9 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   }
   __syncthreads();
   KGE_PROF(2);
+  if constexpr (KGE_FILE_EARLY == 2 && !OWN) {
+    if (active && early) commit_early();
+  }
 
   // ---- merge the positive's waves (one thread per positive)
   if constexpr (OWN) {
@@ -978,7 +1043,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
         // row maximum; general p: p itself)
         A.coef[((uint32_t)i << A.kshift) | (uint32_t)j] =
             make_float2(score_alpha<SK>(c, R, lp, gT[j], A.pw, A.p), SK == SK_PGEN ? A.p : R);
-        bin_key(A, ids[j], ((uint32_t)i << A.kshift) | (uint32_t)j);
+        if (!early) bin_key(A, ids[j], ((uint32_t)i << A.kshift) | (uint32_t)j);
       }
     }
   }
@@ -1801,25 +1866,9 @@ static inline void launch_rel_seg(const StepArgs& A, hipStream_t st) {
   hipLaunchKernelGGL(rel_seg_kernel<0>, grid, dim3(kRsThreads), 0, st, A);
 }
 
-#include "kge_score_pipe.h"
-
 // ------------------------------------------------------------ dispatch
 template <template <int, int, int> class Model, int VEC, int NC, int SK>
 static void launch_score(const StepArgs& A, const StepGeom& G, hipStream_t st) {
-  if constexpr (NC == 1 && pipe_ok<Model<VEC, NC, SK>>::v) {
-    if (A.pipe) {
-      const dim3 grid((unsigned)G.nWG_pipe), blk(kPipeThreads);
-      if (A.side_mode == KGE_SIDE_HT)
-        hipLaunchKernelGGL((score_pipe_kernel<Model, VEC, SK, KGE_SIDE_HT>), grid, blk, G.lds_pipe, st, A);
-#ifndef KGE_ONLY_ONE
-      else if (A.side_mode == KGE_SIDE_H)
-        hipLaunchKernelGGL((score_pipe_kernel<Model, VEC, SK, KGE_SIDE_H>), grid, blk, G.lds_pipe, st, A);
-      else
-        hipLaunchKernelGGL((score_pipe_kernel<Model, VEC, SK, KGE_SIDE_T>), grid, blk, G.lds_pipe, st, A);
-#endif
-      return;
-    }
-  }
 #ifdef KGE_ONLY_ONE
   hipLaunchKernelGGL((score_kernel<Model, VEC, NC, SK, KGE_SIDE_HT>), dim3(G.nWG), dim3(kStepThreads), G.lds_score,
                      st, A);

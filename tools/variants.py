@@ -24,9 +24,15 @@ def build(name, defines, full=False):
                             "kge_owner_transe.hip", "kge_owner_other.hip"), \
             ["-DKGE_ONLY_ONE"] + list(defines)
     for src in sources:
-        obj = "/tmp/var_%s_%s" % (name, src.replace(".hip", ".o"))
-        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"] + defines + \
-              ["-c", os.path.join(CSRC, src), "-o", obj]
+        # single-instance builds: the knobs are the score / update kernels' (kge_step.hip);
+        # the other units are compiled once, shared by every variant
+        shared = not full and src != "kge_step.hip"
+        obj = "/tmp/var_%s_%s" % ("shared" if shared else name, src.replace(".hip", ".o"))
+        if shared and os.path.exists(obj):
+            objs.append(obj)
+            continue
+        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"] + \
+              (["-DKGE_ONLY_ONE"] if shared else defines) + ["-c", os.path.join(CSRC, src), "-o", obj]
         procs.append(subprocess.Popen(cmd))
         objs.append(obj)
     for p in procs:
