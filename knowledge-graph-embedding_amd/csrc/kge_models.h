@@ -411,9 +411,18 @@ struct DistMult {
 
   __device__ static void load_ctx(Ctx& c, const TabView& ent, const TabView& rel, int64_t h,
                                   int64_t r, int64_t t, const MP& mp) {
+    load_ctx_raw(c, ent, rel, h, r, t);
+    ctx_finish(c, mp);
+  }
+  // the two halves (the score kernel's KGE_CTX_LATE): raw rows, then the
+  // normalisation and the products
+  __device__ static void load_ctx_raw(Ctx& c, const TabView& ent, const TabView& rel, int64_t h, int64_t r,
+                                      int64_t t) {
     load_row(c.H, ent.row(h), ent.cols);
     load_row(c.R, rel.row(r), rel.cols);
     load_row(c.T, ent.row(t), ent.cols);
+  }
+  __device__ static void ctx_finish(Ctx& c, const MP& mp) {
     if (mp.norm) {
       normalize_row(c.H);
       normalize_row(c.T);
@@ -500,11 +509,25 @@ struct RotatE {
   struct ECtx { F c0, c1; };
   __device__ static void load_ctx(Ctx& c, const TabView& ent, const TabView& rel, int64_t h,
                                   int64_t r, int64_t t, const MP& mp) {
-    const float limit = mp.limit;
+    load_ctx_raw(c, ent, rel, h, r, t);
+    ctx_finish(c, mp);
+  }
+  // the two halves (the score kernel's KGE_CTX_LATE): the raw rows (the
+  // phases parked in CS's first half), then (cos, sin) and X = H o w
+  __device__ static void load_ctx_raw(Ctx& c, const TabView& ent, const TabView& rel, int64_t h, int64_t r,
+                                      int64_t t) {
     load_row(c.H, ent.row(h), ent.cols);
     load_row(c.T, ent.row(t), ent.cols);
     float ph[HV * NC];
     load_row_half<VEC, NC>(ph, rel.row(r), rel.cols);
+#pragma unroll
+    for (int k = 0; k < HV * NC; ++k) c.CS.v[k] = ph[k];
+  }
+  __device__ static void ctx_finish(Ctx& c, const MP& mp) {
+    const float limit = mp.limit;
+    float ph[HV * NC];
+#pragma unroll
+    for (int k = 0; k < HV * NC; ++k) ph[k] = c.CS.v[k];
 #pragma unroll
     for (int k = 0; k < HV * NC; ++k) {
       const float th = (ph[k] / limit) * kPiF;

@@ -495,6 +495,9 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   auto commit_early = [&]() {
     if (jfile < jend) bin_commit(A, kdest, ((uint32_t)i << A.kshift) | (uint32_t)jfile, kc);
   };
+  // the owner pass's early filing: its two ranges' claims (h-corrupt, t-corrupt)
+  bool early_own = false;
+  KeyClaim kco[2] = {{0u, 0u, 0ull}, {0u, 0u, 0ull}};
   typename M::Ctx ctx;
   float Mrun = -INFINITY, Zs = 0.f, csum = 0.f;
   float nrm[4] = {0.f, 0.f, 0.f, 0.f};
@@ -722,6 +725,21 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
     if constexpr (OWN) {
       stream_lk(std::integral_constant<int, SIDE == KGE_SIDE_HT ? KGE_SIDE_H : SIDE>{}, hb, he);
       if constexpr (SIDE == KGE_SIDE_HT) stream_lk(std::integral_constant<int, KGE_SIDE_T>{}, tb, te);
+      if constexpr (KGE_FILE_EARLY == 2) {
+        // the owned slots' claims (lane l: slot hb + l, slot tb + l), stored
+        // by the finalise pass after the merge
+        const uint32_t kb = __builtin_bit_cast(uint32_t, s_mrg[grp * MG_STRIDE + MG_KB]);
+        early_own = A.train && he - hb <= KGE_WAVE && te - tb <= KGE_WAVE;
+        if (early_own) {
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            const int c = (r ? tb : hb) + lane;
+            if (c < (r ? te : he) && kb + (uint32_t)c < A.own_cap) kco[r] = bin_claim(A, ids[c]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
     } else {
       stream_lk(std::integral_constant<int, SIDE>{}, jbeg, jend);
       if constexpr (LATE) {
@@ -993,7 +1011,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
       const float* mg = s_mrg + grp * MG_STRIDE;
       const float Ms = mg[MG_MS], spv = mg[MG_SP];
       const uint32_t kb = __builtin_bit_cast(uint32_t, mg[MG_KB]);
-      auto fin = [&](int cb, int ce) {
+      auto fin = [&](int cb, int ce, int rng) {
         for (int c = cb + lane; c < ce; c += KGE_WAVE) {
           const float R = gR[c];
           float lp;
@@ -1011,15 +1029,16 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
             const uint32_t kpos = kb + (uint32_t)c;
             if (kpos < A.own_cap) {
               A.own_codes[kpos] = code;
-              bin_key(A, ids[c], code, kpos);
+              if (early_own) bin_commit(A, ids[c], code, kco[rng], kpos);   // (one slot per lane and range)
+              else bin_key(A, ids[c], code, kpos);
             } else if (A.own_err) {
               *A.own_err = 2.f;   // (2: told apart from the exchange plan's block overflow, 1)
             }
           }
         }
       };
-      fin(hb, he);
-      fin(tb, te);
+      fin(hb, he, 0);
+      fin(tb, te, 1);
     }
   } else if (active) {
     const float* mg = s_mrg + grp * MG_STRIDE;
