@@ -483,7 +483,10 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   KGE_PROF(0);
 
   // early filing (KGE_FILE_EARLY): this lane's slot jbeg + lane, its claim
-  const bool early = KGE_FILE_EARLY != 0 && !OWN && A.train && A.SW <= KGE_WAVE;
+  // (not for the wide instances -- rows of two chunks, RotatE, DistMult: their
+  // 2-waves-per-SIMD budget is nearly full and the claims' registers spilled)
+  constexpr bool NARROW = !(NC >= 2 || M::WIDE);
+  const bool early = KGE_FILE_EARLY != 0 && NARROW && !OWN && A.train && A.SW <= KGE_WAVE;
   const int jfile = jbeg + lane;
   int64_t kdest = 0;
   KeyClaim kc{0u, 0u};
@@ -548,7 +551,7 @@ __global__ __launch_bounds__(kStepThreads) __attribute__((amdgpu_waves_per_eu((N
   }
   // KGE_CTX_LATE: the context rows' loads go out now, their combination (and
   // the positive's score) after the first row batch's loads are issued
-  constexpr bool LATE = KGE_CTX_LATE && !OWN && ctx_split<M>::v;
+  constexpr bool LATE = KGE_CTX_LATE && NARROW && !OWN && ctx_split<M>::v;   // (wide instances: it spilled, C3)
   bool ctx_done = !LATE;
   if constexpr (!M::SELF_CTX) {
     if (active) {
