@@ -24,9 +24,10 @@ def build(name, defines, full=False):
                             "kge_owner_transe.hip", "kge_owner_other.hip"), \
             ["-DKGE_ONLY_ONE"] + list(defines)
     for src in sources:
-        # single-instance builds: the knobs are the score / update kernels' (kge_step.hip);
+        # single-instance builds: the knobs are the score / update kernels' (kge_step.hip)
+        # and the plan's (kge_abi.hip: KGE_STEP_WAVES, KGE_SLOTS_PER_WAVE size the launch);
         # the other units are compiled once, shared by every variant
-        shared = not full and src != "kge_step.hip"
+        shared = not full and src not in ("kge_step.hip", "kge_abi.hip")
         obj = "/tmp/var_%s_%s" % ("shared" if shared else name, src.replace(".hip", ".o"))
         if shared and os.path.exists(obj):
             objs.append(obj)
