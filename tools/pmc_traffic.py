@@ -21,7 +21,14 @@ KERNELS = ("score_kernel", "update_kernel", "constrain_rows_kernel", "apply_kern
 
 
 def short(name):
-    for k in KERNELS:
+    # the kernel's own name (kge::<name><...>(...)), else the first listed
+    # substring -- the longest first, so rescal_apply_kernel is not apply_kernel
+    if "kge::" in name:
+        base = name.split("kge::", 1)[1].split("(", 1)[0].split("<", 1)[0]
+        if base.startswith("(anonymous namespace)::"):
+            base = base.split("::", 1)[1]
+        return base
+    for k in sorted(KERNELS, key=len, reverse=True):
         if k in name:
             return k
     return None
