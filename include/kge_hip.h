@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define KGE_ABI_VERSION 7
+#define KGE_ABI_VERSION 8
 
 typedef enum kge_status {
   KGE_OK = 0,
@@ -404,6 +404,15 @@ typedef struct kge_rank_desc {
   int64_t* rank_out;          /* [n]                                            */
   float* pos_score_out;       /* [n] the true triples' scores                   */
   int32_t* status;            /* device status word (nullable)                  */
+  /* ABI 8: the filter as a bitmap (nullable). With a filter and filt_bits,
+   * the library builds bit e of words [q * W, (q + 1) * W), W = ceil(E / 32),
+   * for every entity e of query q's filter list and the count pass skips the
+   * marked candidates, instead of rescoring the filtered entities in a pass
+   * of its own (one workgroup per query: the thousands of known heads of a
+   * popular (r, t) make it the slow tail of the h side). Same ranks bit for
+   * bit. filt_bits_words >= n * W; contents on entry are ignored. */
+  uint32_t* filt_bits;
+  int64_t filt_bits_words;
 } kge_rank_desc;
 
 /* Batched filtered ranking (see kge_rank_desc). */

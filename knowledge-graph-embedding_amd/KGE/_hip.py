@@ -11,7 +11,7 @@ import threading
 
 import torch
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 KGE_OK, KGE_EINVAL, KGE_ERANGE, KGE_EHIP, KGE_ENOMEM_WORKSPACE, KGE_EUNSUPPORTED, KGE_EWORKSPACE = range(7)
 
@@ -103,7 +103,8 @@ class kge_rank_desc(ctypes.Structure):
                 ("idx_dtype", ctypes.c_int32), ("score_kind", ctypes.c_int32), ("score_p", ctypes.c_float),
                 ("flags", ctypes.c_int32), ("n", ctypes.c_int64), ("filt_beg", ctypes.c_void_p),
                 ("filt_end", ctypes.c_void_p), ("filt_ent", ctypes.c_void_p), ("rank_out", ctypes.c_void_p),
-                ("pos_score_out", ctypes.c_void_p), ("status", ctypes.c_void_p)]
+                ("pos_score_out", ctypes.c_void_p), ("status", ctypes.c_void_p), ("filt_bits", ctypes.c_void_p),
+                ("filt_bits_words", ctypes.c_int64)]
 
 
 class kge_apply_rows_desc(ctypes.Structure):

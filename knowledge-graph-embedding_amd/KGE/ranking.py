@@ -294,6 +294,10 @@ def cached_filter_keys(positive_X, side, E, dev):
 
 
 # ---------------------------------------------------------------- entry
+_BITS_MAX_BYTES = 1 << 30
+RESCORE_FILTER = 1 << 30   # (batched_ranks flag, not passed on: the rescoring filter pass, for A/B tests)
+
+
 def batched_ranks(model, eval_X, corrupt_side, positive_X=None, flags=0):
     """Ranks of every triple of ``eval_X`` (numpy int64 [n]), the same values
     ``get_rank`` gives one triple at a time. ``flags``: KGE_RANK_FLAG_*."""
@@ -318,6 +322,13 @@ def batched_ranks(model, eval_X, corrupt_side, positive_X=None, flags=0):
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     true_col = 0 if corrupt_side == "h" else 2
     keep = []
+    # the filter as a bitmap (ABI 8: the count pass skips the known positives,
+    # no rescoring pass), n x ceil(E / 32) words while that stays under
+    # _BITS_MAX_BYTES; past it the library's rescoring filter pass runs
+    bits = None
+    W = (E + 31) // 32
+    if positive_X is not None and not (flags & RESCORE_FILTER) and 0 < n * W * 4 <= _BITS_MAX_BYTES:
+        bits = torch.empty(n * W, dtype=torch.int32, device=dev)
     for g in groups:
         sel = g["sel"]
         ids = X[:, true_col] if sel is None else X[sel, true_col]
@@ -346,11 +357,13 @@ def batched_ranks(model, eval_X, corrupt_side, positive_X=None, flags=0):
         d.idx_dtype = _hip.IDX_I64
         d.score_kind, d.score_p = g["score"]
         d.n = m
-        d.flags = int(flags)
+        d.flags = int(flags) & ~RESCORE_FILTER
         if positive_X is not None:
             gb = fb if sel is None else fb[sel].contiguous()
             ge = fe if sel is None else fe[sel].contiguous()
             d.filt_beg, d.filt_end, d.filt_ent = gb.data_ptr(), ge.data_ptr(), fent.data_ptr()
+            if bits is not None:
+                d.filt_bits, d.filt_bits_words = bits.data_ptr(), bits.numel()
             keep.append((gb, ge))
         d.rank_out = rk.data_ptr()
         d.pos_score_out = ps.data_ptr()

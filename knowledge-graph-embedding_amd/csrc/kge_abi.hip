@@ -1068,6 +1068,14 @@ kge_status kge_rank(const kge_rank_desc* d, void* stream) {
   A.fbeg = d->filt_beg;
   A.fend = d->filt_end;
   A.fent = d->filt_ent;
+  if (d->filt_bits && d->filt_beg) {   // (no filter: the bitmap is ignored)
+    A.fw = (A.E + 31) / 32;
+    if (d->filt_bits_words < d->n * A.fw)
+      return fail(KGE_EINVAL, "filt_bits: %lld words < n * ceil(E / 32) = %lld", (long long)d->filt_bits_words,
+                  (long long)(d->n * A.fw));
+    if (d->n > 0x7fffffffLL) return fail(KGE_EINVAL, "filt_bits: more than 2^31 - 1 queries per call");
+    A.fbits = d->filt_bits;
+  }
   A.rank = (unsigned long long*)d->rank_out;
   A.pos = d->pos_score_out;
   A.status = d->status;

@@ -19,6 +19,11 @@
 //   rank_filter_kernel  wave per query: rescores only its filtered entities
 //                       and subtracts those above the true score, + 1
 //
+// With a filter bitmap (kge_rank_desc.filt_bits, ABI 8) rank_bits_kernel
+// marks each query's filtered entities first, the count passes skip marked
+// candidates and the pos pass starts every rank at 1: no rescoring pass. The
+// comparisons are the same ones, so are the ranks.
+//
 // Every score is evaluated op by op (no contraction) in one fixed order, so
 // the true entity scored as a candidate equals its pos score bit for bit and
 // never counts itself, and the filter pass sees exactly the scores the count
@@ -166,6 +171,36 @@ __global__ __launch_bounds__(256) void rank_pos_kernel(RankArgs A) {
   float o[1];
   rank_scores<MODE, PJ, SK, 1>(A, e, qrow(A.q0, A, q), qrow(A.q1, A, q), qrow(A.qw, A, q), 0, o);
   A.pos[q] = o[0];
+  if (A.fbits) A.rank[q] = 1ull;   // (bitmap filter: the +1 of the filter pass; counts are added after)
+}
+
+// The filter bitmap: workgroup per query, bit e of the query's words for each
+// entity of its filter list (sorted, unique per query; an id outside [0, E)
+// sets KGE_ERANGE). Up to kBitsLds words per query the bits are gathered in
+// LDS and every word is written once (no clear needed); past that the caller
+// (kge_rank) clears the words first and the bits go in with global atomics.
+constexpr int kBitsLds = 8192;
+template <bool LDS>
+__global__ __launch_bounds__(256) void rank_bits_kernel(RankArgs A, uint32_t* bits) {
+  __shared__ uint32_t sb[LDS ? kBitsLds : 1];
+  const int64_t q = blockIdx.x;
+  const int W = (int)A.fw;
+  uint32_t* out = bits + q * A.fw;
+  if (LDS) {
+    for (int w = threadIdx.x; w < W; w += 256) sb[w] = 0u;
+    __syncthreads();
+  }
+  for (int64_t j = A.fbeg[q] + threadIdx.x; j < A.fend[q]; j += 256) {
+    const int64_t e = load_idx(A.fent, j, A.i64);
+    if (e < 0 || e >= A.E) { set_status(A.status, KGE_ERANGE); continue; }
+    const uint32_t m = 1u << (uint32_t)(e & 31);
+    if (LDS) atomicOr(&sb[e >> 5], m);
+    else atomicOr(&out[e >> 5], m);
+  }
+  if (LDS) {
+    __syncthreads();
+    for (int w = threadIdx.x; w < W; w += 256) out[w] = sb[w];
+  }
 }
 
 template <int MODE, int PJ, int SK>
@@ -195,11 +230,15 @@ __global__ __launch_bounds__(kRankThreads) void rank_count_kernel(RankArgs A, in
   const int64_t e = ch * kRankThreads + threadIdx.x;
   const bool in = e < A.E;
   const int64_t ee = in ? e : 0;
+  bool keep[kRankQ];   // (bitmap filter: the candidate is not a known positive of the query)
+#pragma unroll
+  for (int q = 0; q < kRankQ; ++q)
+    keep[q] = !(A.fbits && q < nq && ((A.fbits[(q0i + q) * A.fw + (ee >> 5)] >> (uint32_t)(ee & 31)) & 1u));
   float s[kRankQ];
   rank_scores<MODE, PJ, SK, kRankQ>(A, ee, s0, s1, sw, LQ, s);
 #pragma unroll
   for (int q = 0; q < kRankQ; ++q) {
-    const unsigned long long m = __ballot(in && q < nq && s[q] > pos[q]);
+    const unsigned long long m = __ballot(in && q < nq && keep[q] && s[q] > pos[q]);
     if (lane_id() == 0 && m) atomicAdd(&A.rank[q0i + q], (unsigned long long)__popcll(m));
   }
 }
@@ -259,6 +298,16 @@ __global__ __launch_bounds__(256) void rank_tile_kernel(RankArgs A, int64_t qt0)
   const int sr = tid >> 2, se = (tid & 3) * 4;
   const int64_t qr = q0i + sr, er = c0 + sr;
   const bool qv = qr < A.n, ev = er < A.E;
+  // bitmap filter: the word holding this thread's four candidates, per query
+  // (c0 is a multiple of 64, so 4 tc .. 4 tc + 3 share one word)
+  uint32_t fmask[4] = {0u, 0u, 0u, 0u};
+  if (A.fbits && c0 + 4 * tc < A.E) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t q = q0i + 4 * tq + i;
+      if (q < A.n) fmask[i] = A.fbits[q * A.fw + ((c0 + 4 * tc) >> 5)] >> (uint32_t)((4 * tc) & 31);
+    }
+  }
   for (int e0 = 0; e0 < D; e0 += kRC) {
     const int ne = min(kRC, D - e0);
     float a[4], b[4], x[4];
@@ -332,7 +381,7 @@ __global__ __launch_bounds__(256) void rank_tile_kernel(RankArgs A, int64_t qt0)
         float lpv;
         sc = score_value<SK>(av, A.pw, &lpv, A.p);
       }
-      cnt += (c0 + 4 * tc + j < A.E && sc > pv) ? 1u : 0u;
+      cnt += (c0 + 4 * tc + j < A.E && sc > pv && !((fmask[i] >> j) & 1u)) ? 1u : 0u;
     }
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) cnt += (unsigned)__shfl_xor((int)cnt, o, KGE_WAVE);
@@ -424,6 +473,7 @@ __global__ __launch_bounds__(256) void rank_filter_tile_kernel(RankArgs A) {
 template <int MODE, int PJ, int SK>
 static void rank_launch(const RankArgs& A, hipStream_t st) {
   hipLaunchKernelGGL((rank_pos_kernel<MODE, PJ, SK>), dim3((unsigned)((A.n + 255) / 256)), dim3(256), 0, st, A);
+  const bool bits = A.fbits != nullptr;   // (the bitmap was built by launch_rank; no filter pass)
   if constexpr ((MODE == KGE_RANK_TRANS && PJ == KGE_RPROJ_NONE) || MODE == KGE_RANK_MUL || MODE == KGE_RANK_DOT) {
     const int64_t nct = (A.E + kRT - 1) / kRT, nqt = (A.n + kRT - 1) / kRT;
     constexpr int64_t kMaxY = 65535;
@@ -433,7 +483,7 @@ static void rank_launch(const RankArgs& A, hipStream_t st) {
         if (A.hside) hipLaunchKernelGGL((rank_tile_kernel<MODE, SK, true>), grid, dim3(256), 0, st, A, t0);
         else hipLaunchKernelGGL((rank_tile_kernel<MODE, SK, false>), grid, dim3(256), 0, st, A, t0);
       }
-      hipLaunchKernelGGL((rank_filter_tile_kernel<MODE, SK>), dim3((unsigned)A.n), dim3(256), 0, st, A);
+      if (!bits) hipLaunchKernelGGL((rank_filter_tile_kernel<MODE, SK>), dim3((unsigned)A.n), dim3(256), 0, st, A);
       return;
     }
   }
@@ -447,7 +497,7 @@ static void rank_launch(const RankArgs& A, hipStream_t st) {
       hipLaunchKernelGGL((rank_count_kernel<MODE, PJ, SK>),
                          dim3((unsigned)std::min(ng - g0, kMaxX), (unsigned)std::min(nchunk - c0, kMaxY)),
                          dim3(kRankThreads), lds, st, A, g0, c0);
-  hipLaunchKernelGGL((rank_filter_kernel<MODE, PJ, SK>), dim3((unsigned)((A.n + 3) / 4)), dim3(256), 0, st, A);
+  if (!bits) hipLaunchKernelGGL((rank_filter_kernel<MODE, PJ, SK>), dim3((unsigned)((A.n + 3) / 4)), dim3(256), 0, st, A);
 }
 
 template <int MODE, int PJ>
@@ -462,6 +512,15 @@ static void rank_by_sk(const RankArgs& A, int sk, hipStream_t st) {
 }
 
 kge_status launch_rank(const RankArgs& A, int mode, int proj, int sk, hipStream_t st) {
+  if (A.fbits) {   // the filter bitmap, before the passes that read it
+    uint32_t* bits = const_cast<uint32_t*>(A.fbits);
+    if (A.fw <= kBitsLds) {
+      hipLaunchKernelGGL(rank_bits_kernel<true>, dim3((unsigned)A.n), dim3(256), 0, st, A, bits);
+    } else {
+      (void)hipMemsetAsync(bits, 0, (size_t)(A.n * A.fw) * sizeof(uint32_t), st);
+      hipLaunchKernelGGL(rank_bits_kernel<false>, dim3((unsigned)A.n), dim3(256), 0, st, A, bits);
+    }
+  }
   switch (mode) {
     case KGE_RANK_TRANS:
       if (proj == KGE_RPROJ_HYPER) rank_by_sk<KGE_RANK_TRANS, KGE_RPROJ_HYPER>(A, sk, st);

@@ -426,6 +426,7 @@ struct RankArgs {
   const float* q0; const float* q1; const float* qw; int64_t ldq;
   const void* true_ids; bool i64; int64_t n;
   const int64_t* fbeg; const int64_t* fend; const void* fent;
+  const uint32_t* fbits; int64_t fw;       // filter bitmap (ABI 8): query q's words at q * fw, or null
   unsigned long long* rank;
   float* pos;
   int32_t* status;

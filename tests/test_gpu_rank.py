@@ -126,7 +126,9 @@ def test_rank_tiled_pass_equals_lane_pass(name, si):
     """The register-tiled count pass and the lane-per-candidate pass score with
     the same ops in the same order: identical ranks, integer for integer, on a
     FB15k-237-sized candidate set (E = 14,541) with 333 queries per side,
-    filtered by the whole training set -- including ranks decided by ties."""
+    filtered by the whole training set -- including ranks decided by ties.
+    Each pass with the filter as a bitmap (the default, ABI 8) and with the
+    rescoring filter pass: the same four rank vectors."""
     from KGE import _hip, ranking, score
     from tests.test_plugin_surface import build
     z = np.load(os.path.join(ROOT, "data", "fb15k237_train.npz"))
@@ -150,6 +152,68 @@ def test_rank_tiled_pass_equals_lane_pass(name, si):
         tiled = ranking.batched_ranks(m, X, side, PX)
         lane = ranking.batched_ranks(m, X, side, PX, flags=_hip.RANK_FLAG_LANE_PASS)
         assert np.array_equal(tiled, lane), np.nonzero(tiled != lane)[0][:10]
+        for f in (ranking.RESCORE_FILTER, ranking.RESCORE_FILTER | _hip.RANK_FLAG_LANE_PASS):
+            rs = ranking.batched_ranks(m, X, side, PX, flags=f)
+            assert np.array_equal(tiled, rs), (f, np.nonzero(tiled != rs)[0][:10])
+
+
+def test_rank_filter_bitmap_abi():
+    """kge_rank's bitmap filter through the C-ABI: a bitmap shorter than
+    n * ceil(E / 32) words is refused; an out-of-range filter id sets
+    KGE_ERANGE in the status word (as the rescoring pass does); words past a
+    query's filter are cleared whatever the buffer held."""
+    import ctypes
+    from KGE import _hip
+    dev = torch.device("cuda", 0)
+    E, D, n = 70, 8, 3
+    g = torch.Generator().manual_seed(3)
+    cand = torch.rand(E, D, generator=g).to(dev)
+    q0 = torch.rand(n, D, generator=g).to(dev)
+    ids = torch.tensor([1, 5, 69], dtype=torch.int64, device=dev)
+    fent = torch.tensor([1, 2, 40, 5, 69, 0], dtype=torch.int64, device=dev)
+    fb = torch.tensor([0, 3, 4], dtype=torch.int64, device=dev)
+    fe = torch.tensor([3, 4, 6], dtype=torch.int64, device=dev)
+    W = (E + 31) // 32
+    bits = torch.full((n * W,), -1, dtype=torch.int32, device=dev)
+    rk = torch.zeros(n, dtype=torch.int64, device=dev)
+    ps = torch.zeros(n, dtype=torch.float32, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    d = _hip.kge_rank_desc()
+    d.abi_version = _hip.ABI_VERSION
+    d.mode, d.proj, d.corrupt_side = _hip.RANK_TRANS, _hip.RPROJ_NONE, _hip.SIDE_T
+    d.cand = _hip.table(cand)
+    d.dim = D
+    d.q0, d.ldq = q0.data_ptr(), D
+    d.true_ids, d.idx_dtype = ids.data_ptr(), _hip.IDX_I64
+    d.score_kind, d.score_p = 0, 2.0   # KGE_SCORE_LP
+    d.n = n
+    d.filt_beg, d.filt_end, d.filt_ent = fb.data_ptr(), fe.data_ptr(), fent.data_ptr()
+    d.rank_out, d.pos_score_out, d.status = rk.data_ptr(), ps.data_ptr(), status.data_ptr()
+    d.filt_bits, d.filt_bits_words = bits.data_ptr(), n * W - 1
+    lib = _hip.lib()
+    assert lib.kge_rank(ctypes.byref(d), _hip.stream_handle(dev)) == _hip.KGE_EINVAL
+    d.filt_bits_words = n * W
+    assert lib.kge_rank(ctypes.byref(d), _hip.stream_handle(dev)) == _hip.KGE_OK
+    torch.cuda.synchronize()
+    got = bits.view(n, W).cpu().numpy().view(np.uint32)
+    want = np.zeros((n, W), dtype=np.uint32)
+    for q, ents in enumerate([[1, 2, 40], [5], [69, 0]]):
+        for e in ents:
+            want[q, e >> 5] |= np.uint32(1 << (e & 31))
+    assert np.array_equal(got, want)
+    assert int(status.item()) == 0
+    # the ranks with and without the bitmap
+    with_bits = rk.cpu().numpy().copy()
+    d.filt_bits, d.filt_bits_words = None, 0
+    assert lib.kge_rank(ctypes.byref(d), _hip.stream_handle(dev)) == _hip.KGE_OK
+    torch.cuda.synchronize()
+    assert np.array_equal(with_bits, rk.cpu().numpy())
+    # an id past the table
+    fent[2] = E
+    d.filt_bits, d.filt_bits_words = bits.data_ptr(), n * W
+    assert lib.kge_rank(ctypes.byref(d), _hip.stream_handle(dev)) == _hip.KGE_OK
+    torch.cuda.synchronize()
+    assert int(status.item()) == _hip.KGE_ERANGE
 
 
 def _oracle_weights(m):
