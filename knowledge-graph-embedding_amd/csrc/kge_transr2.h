@@ -815,6 +815,7 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
 
     if (mv4) gemm2(std::false_type{}, std::true_type{});
     else gemm2(std::false_type{}, std::false_type{});
+    KGE_PROF(43);
     // ---- GEMM3: dM_i = X^T S' + x_h^T (sum of h slices) + x_t^T (sum of t slices)
     // (S' rows in LDS, X re-read from the table: L2; the rank-2 part in the
     // epilogue); job = 16-row tile of dM (its A column in registers) x a pair of

@@ -23,8 +23,10 @@ LIB = os.path.join(PKG, "KGE", "_lib", "libkge_hip_trprof.so")
 PHASES = {32: "ids", 33: "gather X", 34: "row stats + GEMM1", 35: "clip", 36: "scores", 37: "loss coefs",
           38: "grads (regs)", 39: "S rows + sums", 40: "GEMM2", 41: "GEMM3", 42: "keys"}
 # transr2_kernel (two per CU, the default; --v1 times transr_kernel)
+# (in execution order: KGE_PROF(k) in csrc/kge_transr2.h closes the phase named here)
 PHASES2 = {32: "ids", 33: "gather X", 34: "row stats + GEMM1", 35: "clip + h/t rows", 36: "scores", 37: "loss coefs",
-           38: "passes A-C", 39: "S' rows + GEMM2", 40: "GEMM3", 41: "Q rows + GEMM2 norms", 42: "keys"}
+           38: "passes A-C", 39: "(drain)", 40: "Q rows + GEMM2 norms", 43: "S' rows + GEMM2",
+           41: "GEMM3 + dM stores", 42: "keys"}
 
 
 def build():
