@@ -615,6 +615,9 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
       const float htx = kind == KIND_TC ? xh[row] : kind == KIND_HC ? xt[row] : xh[TR];
       return hx * (Gx * Gx) + tx * (Gy * Gy) + 2.f * htx * (Gx * Gy);
     };
+    // The Q rows (negative q's positive-side slice, GEMM2's norm pass) go to
+    // LDS as they are computed, over X (dead since GEMM1, several barriers
+    // ago): rows without a triple and columns past k as zeros
 #pragma unroll
     for (int rt = 0; rt < 5; ++rt) {
 #pragma unroll
@@ -624,15 +627,18 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
       for (int j = 0; j < 4; ++j) {
         const int row = rt * 16 + g4 + j;
         const int kind = rkind(row);
-        if (kind < 0) continue;
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-          if (!live(u)) continue;
-          float E, Q, Gx, Gy;
-          slices(u, P[u][rt][j], row, kind, E, Q, Gx, Gy);
-          n_proj += nproj(row, kind, Gx, Gy);
-          if (kind != KIND_HC) sh[u] += Q; else st[u] += Q;
-          SP[u][rt][j] = E;
+          if (!has(u)) continue;
+          float Q = 0.f;
+          if (kind >= 0 && colu[u] < k) {
+            float E, Gx, Gy;
+            slices(u, P[u][rt][j], row, kind, E, Q, Gx, Gy);
+            n_proj += nproj(row, kind, Gx, Gy);
+            if (kind != KIND_HC) sh[u] += Q; else st[u] += Q;
+            SP[u][rt][j] = E;
+          }
+          X[row * LX + colu[u]] = Q;
         }
       }
     }
@@ -673,32 +679,13 @@ __global__ __launch_bounds__(kTrThreads) __attribute__((amdgpu_waves_per_eu(4)))
     // written above are read by GEMM2, after the barrier that ends the staging)
     KGE_PROF(39);
     load_rows();
-    // ---- Q rows: negative q's positive-side slice -> GEMM2's norms
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      if (!has(u)) continue;
-#pragma unroll
-      for (int rt = 0; rt < 5; ++rt) {
-        if (rt >= nrt) break;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = rt * 16 + g4 + j;
-          const int kind = rkind(row);
-          float val = 0.f;
-          if (colu[u] < k && kind >= 0) {
-            float E, Q, Gx, Gy;
-            slices(u, P[u][rt][j], row, kind, E, Q, Gx, Gy);
-            val = Q;
-          }
-          X[row * LX + colu[u]] = val;
-        }
-      }
-    }
+    // (the Q rows were written by pass B)
     {   // (columns past P's tiles: zero, as the S' rows below)
       const int c0 = 16 * nct, wpad = W - c0;
       for (int e = tid; e < NR16 * wpad; e += kTrThreads) X[(e / wpad) * LX + c0 + e % wpad] = 0.f;
     }
     __syncthreads();
+    KGE_PROF(44);
     // ---- GEMM2: Y = S M_r^T over the staged rows; job = one 16-column tile of
     // Y (d) over every row tile, M_r^T's column streamed chunk by chunk (two
     // chunks ahead). Two k-vectors ride on the same column (VALU): NORMS = false:

@@ -25,7 +25,7 @@ PHASES = {32: "ids", 33: "gather X", 34: "row stats + GEMM1", 35: "clip", 36: "s
 # transr2_kernel (two per CU, the default; --v1 times transr_kernel)
 # (in execution order: KGE_PROF(k) in csrc/kge_transr2.h closes the phase named here)
 PHASES2 = {32: "ids", 33: "gather X", 34: "row stats + GEMM1", 35: "clip + h/t rows", 36: "scores", 37: "loss coefs",
-           38: "passes A-C", 39: "(drain)", 40: "Q rows + GEMM2 norms", 43: "S' rows + GEMM2",
+           38: "passes A-C", 39: "(drain)", 44: "Q rows + barrier", 40: "GEMM2 norms", 43: "S' rows + GEMM2",
            41: "GEMM3 + dM stores", 42: "keys"}
 
 
