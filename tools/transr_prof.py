@@ -19,7 +19,7 @@ for p in (ROOT, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 CSRC = os.path.join(PKG, "csrc")
-LIB = os.path.join(PKG, "KGE", "_lib", "libkge_hip_trprof.so")
+LIB = os.path.join(PKG, "KGE", "_lib", os.environ.get("KGE_TRPROF_LIB", "libkge_hip_trprof.so"))
 PHASES = {32: "ids", 33: "gather X", 34: "row stats + GEMM1", 35: "clip", 36: "scores", 37: "loss coefs",
           38: "grads (regs)", 39: "S rows + sums", 40: "GEMM2", 41: "GEMM3", 42: "keys"}
 # transr2_kernel (two per CU, the default; --v1 times transr_kernel)
@@ -29,7 +29,7 @@ PHASES2 = {32: "ids", 33: "gather X", 34: "row stats + GEMM1", 35: "clip + h/t r
            41: "GEMM3 + dM stores", 42: "keys"}
 
 
-def build():
+def build(extra=()):
     """The library's objects as build() made them, with kge_transr.hip and the
     P2 unit of kge_transr2 recompiled with -DKGE_PHASE_PROF."""
     import __graft_entry__ as g
@@ -41,7 +41,7 @@ def build():
             objs.append(os.path.join(ROOT, "build", "obj", "%s.%s.o" % (src[:-4], g._obj_key(src))))
             continue
         obj = os.path.join("/tmp", "trprof_" + src.replace(".hip", ".o"))
-        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DKGE_PHASE_PROF",
+        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-DKGE_PHASE_PROF"] + list(extra) + [
                "-c", os.path.join(CSRC, src), "-o", obj]
         procs.append(subprocess.Popen(cmd))
         objs.append(obj)
