@@ -1192,9 +1192,12 @@ void update_kernel(StepArgs A) {
   using M = Model<VEC, NC, SK>;
   using F = Frag<VEC, NC>;
   // entries in flight per wave; the compact instance (8 waves / SIMD: 64
-  // VGPRs) takes 4 -- 8 spilled 28 bytes per lane (C2-50M KU 170 -> 160 us)
+  // VGPRs) takes 4 -- 8 spilled 28 bytes per lane (C2-50M KU 170 -> 160 us).
+  // Rows of two or more fragment chunks (RotatE d = 256, TransE d = 512) keep
+  // two: four made C3's KU 79 -> 100.5 us (register-bound occupancy,
+  // profiles/r06z), eight 138 us
   constexpr int UU = UW >= 8 ? 4 : KGE_UPDATE_U;
-  constexpr int U = UU / NC > 1 ? UU / NC : 2;
+  constexpr int U = NC >= 2 ? 2 : (UU > 1 ? UU : 2);
   constexpr int RV = RelV<M::CPLX, VEC>::n;
   constexpr int CHMAX = 4;                            // in-register ordering up to 256 codes
   __shared__ uint32_t s_scr[kUpdWaves][CHMAX * KGE_WAVE];
