@@ -42,6 +42,9 @@
 #ifndef KGE_UPD_COMPACT_WPE
 #define KGE_UPD_COMPACT_WPE 8   // compact update launch: amdgpu_waves_per_eu (tuning knob)
 #endif
+#ifndef KGE_UPD_WIDE_WPE
+#define KGE_UPD_WIDE_WPE 1      // update launches of wide rows (NC >= 2 or WIDE): amdgpu_waves_per_eu (tuning knob)
+#endif
 #ifndef KGE_COMPACT_LIST0
 #define KGE_COMPACT_LIST0 1 // compact launches: list position 0 lives only in the leader table (A-B knob)
 #endif
@@ -1920,7 +1923,11 @@ static kge_status launch_family(const StepArgs& A, const StepGeom& G, hipStream_
         hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK, KGE_UPD_COMPACT_WPE, true>), dim3(G.gridU),
                            dim3(kUpdThreads), 0, st, A);
       else
-        hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK, 1, true>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
+        hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK, KGE_UPD_WIDE_WPE, true>), dim3(G.gridU),
+                           dim3(kUpdThreads), 0, st, A);
+    } else if constexpr (NC >= 2 || Model<VEC, NC, SK>::WIDE) {
+      hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK, KGE_UPD_WIDE_WPE>), dim3(G.gridU), dim3(kUpdThreads), 0,
+                         st, A);
     } else {
       hipLaunchKernelGGL((update_kernel<Model, VEC, NC, SK>), dim3(G.gridU), dim3(kUpdThreads), 0, st, A);
     }
