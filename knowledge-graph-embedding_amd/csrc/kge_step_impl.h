@@ -42,6 +42,9 @@
 #ifndef KGE_UPD_COMPACT_WPE
 #define KGE_UPD_COMPACT_WPE 8   // compact update launch: amdgpu_waves_per_eu (tuning knob)
 #endif
+#ifndef KGE_UPD_COMPACT_U
+#define KGE_UPD_COMPACT_U 4     // compact update launch (8 waves / SIMD): entries in flight (tuning knob)
+#endif
 #ifndef KGE_UPD_WIDE_WPE
 #define KGE_UPD_WIDE_WPE 1      // update launches of wide rows (NC >= 2 or WIDE): amdgpu_waves_per_eu (tuning knob)
 #endif
@@ -1199,7 +1202,7 @@ void update_kernel(StepArgs A) {
   // Rows of two or more fragment chunks (RotatE d = 256, TransE d = 512) keep
   // two: four made C3's KU 79 -> 100.5 us (register-bound occupancy,
   // profiles/r06z), eight 138 us
-  constexpr int UU = UW >= 8 ? 4 : KGE_UPDATE_U;
+  constexpr int UU = UW >= 8 ? KGE_UPD_COMPACT_U : KGE_UPDATE_U;
   constexpr int U = NC >= 2 ? 2 : (UU > 1 ? UU : 2);
   constexpr int RV = RelV<M::CPLX, VEC>::n;
   constexpr int CHMAX = 4;                            // in-register ordering up to 256 codes
